@@ -1,0 +1,244 @@
+"""Device engine around libhmmbw: one context per (GPU, model shape), data-parallel over ranks.
+
+Single rank: iterations are enqueued in chunks with ``hmmbw_iterate`` (E-step kernel + M-step kernel
+per iteration, no host round trip); the host synchronises once per chunk to read the convergence
+records.  Iterations enqueued after convergence are device-side no-ops, so the result is exactly
+the reference's stop rule (hmm_training.py:346).
+
+Multiple ranks (one process per GPU, torch.distributed over RCCL): every rank owns a contiguous,
+length-balanced shard of the sequences; per iteration it runs the E-step on its shard, the packed
+fp64 statistics are summed with ONE all-reduce, and every rank runs the identical M-step, so the
+parameters and the convergence decision stay replicated without a broadcast.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Callable, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from ._lib import TOPOLOGY, TOPOLOGY_NAME, IterRecord, Status, check, lib
+
+IterCallback = Callable[[int, float, float], None]
+
+
+def to_csr(observations: Sequence[np.ndarray]) -> Tuple[np.ndarray, np.ndarray]:
+    """Ragged list of symbol arrays -> (offsets int64 [R+1], symbols int32 [sum T])."""
+    arrs = [np.asarray(o).reshape(-1) for o in observations]
+    lengths = np.fromiter((a.size for a in arrs), dtype=np.int64, count=len(arrs))
+    offsets = np.zeros(len(arrs) + 1, dtype=np.int64)
+    np.cumsum(lengths, out=offsets[1:])
+    if len(arrs) and offsets[-1] > 0:
+        sym = np.concatenate(arrs)
+    else:
+        sym = np.zeros(0, dtype=np.int64)
+    if sym.size and not np.issubdtype(sym.dtype, np.integer):
+        if not np.all(np.equal(np.mod(sym, 1), 0)):
+            raise IndexError("observation symbols must be integers")
+    return offsets, np.ascontiguousarray(sym, dtype=np.int32)
+
+
+def shard_bounds(lengths: Sequence[int], world: int) -> List[Tuple[int, int]]:
+    """Contiguous, length-balanced [start, end) shards of a sequence list (one per rank)."""
+    lengths = np.asarray(lengths, dtype=np.int64)
+    R = len(lengths)
+    if world <= 1:
+        return [(0, R)]
+    cum = np.concatenate([[0], np.cumsum(lengths)])
+    total = cum[-1]
+    cuts = [0]
+    for k in range(1, world):
+        target = total * k / world
+        idx = int(np.searchsorted(cum, target))
+        if idx > 0 and abs(cum[idx - 1] - target) <= abs(cum[min(idx, R)] - target):
+            idx -= 1
+        idx = min(max(idx, cuts[-1]), R)
+        cuts.append(idx)
+    cuts.append(R)
+    return [(cuts[i], cuts[i + 1]) for i in range(world)]
+
+
+class StatsLayout:
+    """Packed fp64 statistics buffer of hmmbw_estep/hmmbw_mstep (include/hmmbw.h):
+    [pi_num N][S N*N][gamma_den_excl_last N][gamma_den_all N][B_num M*N (symbol-major)][(m, s) x world].
+    S_ij = sum_t alpha_hat_t(i) v_{t+1}(j), so the reference's xi numerator (hmm_training.py:443-455)
+    is a_ij * S_ij; (m, s) is a rank's (max_r log P_r, sum_r exp(log P_r - m)) pair."""
+
+    def __init__(self, N: int, M: int, world: int = 1):
+        self.N, self.M, self.world = N, M, world
+        self.pi = 0
+        self.S = N
+        self.gex = N + N * N
+        self.gall = self.gex + N
+        self.bnum = self.gall + N
+        self.ll = self.bnum + M * N
+        self.length = self.ll + 2 * world
+
+    def decode(self, buf: np.ndarray) -> dict:
+        N, M = self.N, self.M
+        buf = np.asarray(buf, dtype=np.float64)
+        return dict(pi_num=buf[: N], S=buf[self.S: self.S + N * N].reshape(N, N),
+                    gamma_den_excl=buf[self.gex: self.gex + N], gamma_den_all=buf[self.gall: self.gall + N],
+                    B_num=buf[self.bnum: self.bnum + M * N].reshape(M, N).T,
+                    ll_pairs=buf[self.ll: self.ll + 2 * self.world].reshape(self.world, 2))
+
+    @staticmethod
+    def lse_of_pairs(pairs: np.ndarray) -> float:
+        """L = LSE over all ranks' sequences from the per-rank (m, s) slots (mirrors k_mstep)."""
+        pairs = np.asarray(pairs, dtype=np.float64).reshape(-1, 2)
+        live = pairs[:, 1] > 0
+        if not np.any(live):
+            return float("-inf")
+        m = np.max(pairs[live, 0])
+        return float(m + np.log(np.sum(pairs[live, 1] * np.exp(pairs[live, 0] - m))))
+
+
+def default_device() -> int:
+    if torch.cuda.is_available():
+        return torch.cuda.current_device()
+    return 0
+
+
+class BaumWelchEngine:
+    """Baum-Welch training / scoring of one discrete HMM (N states, M symbols) on one GPU."""
+
+    def __init__(self, n_states: int, n_symbols: int, device: Optional[int] = None, topology: str = "auto",
+                 rank: int = 0, world_size: int = 1, stream: Optional[int] = None):
+        self._lib = lib()
+        self.N, self.M = int(n_states), int(n_symbols)
+        self.device = default_device() if device is None else int(device)
+        self.rank, self.world_size = int(rank), int(world_size)
+        ctx = ctypes.c_void_p()
+        check(self._lib.hmmbw_ctx_create(self.device, self.N, self.M, ctypes.byref(ctx)))
+        self._ctx = ctx
+        if stream is None and torch.cuda.is_available():
+            stream = torch.cuda.current_stream(self.device).cuda_stream
+        if stream is not None:
+            check(self._lib.hmmbw_set_stream(self._ctx, ctypes.c_void_p(stream)))
+        if self.world_size > 1:
+            check(self._lib.hmmbw_set_rank(self._ctx, self.rank, self.world_size))
+        check(self._lib.hmmbw_set_topology(self._ctx, TOPOLOGY[topology]))
+        self.n_seq = 0
+        self.n_seq_global = 0
+
+    # -------------------------------------------------------------------------------- set-up
+    def set_observations(self, observations: Sequence[np.ndarray] = None, offsets: np.ndarray = None,
+                         symbols: np.ndarray = None, n_seq_global: Optional[int] = None) -> None:
+        if observations is not None:
+            offsets, symbols = to_csr(observations)
+        offsets = np.ascontiguousarray(offsets, dtype=np.int64)
+        symbols = np.ascontiguousarray(symbols, dtype=np.int32)
+        R = len(offsets) - 1
+        check(self._lib.hmmbw_set_observations(self._ctx, offsets.ctypes.data, symbols.ctypes.data, R))
+        self.n_seq = R
+        self.n_seq_global = R if n_seq_global is None else int(n_seq_global)
+
+    def set_params(self, pi: np.ndarray, A: np.ndarray, B: np.ndarray) -> None:
+        pi = np.ascontiguousarray(pi, dtype=np.float64).reshape(self.N)
+        A = np.ascontiguousarray(A, dtype=np.float64).reshape(self.N, self.N)
+        B = np.ascontiguousarray(B, dtype=np.float64).reshape(self.N, self.M)
+        check(self._lib.hmmbw_set_params(self._ctx, pi.ctypes.data, A.ctypes.data, B.ctypes.data))
+
+    @property
+    def topology(self) -> str:
+        out = ctypes.c_int()
+        check(self._lib.hmmbw_get_topology(self._ctx, ctypes.byref(out)))
+        return TOPOLOGY_NAME[out.value]
+
+    @property
+    def stats_len(self) -> int:
+        n = ctypes.c_int64()
+        check(self._lib.hmmbw_stats_len(self._ctx, ctypes.byref(n)))
+        return n.value
+
+    # -------------------------------------------------------------------------------- training
+    def reset(self, epsilon: float, max_iterations: int) -> None:
+        check(self._lib.hmmbw_reset_training(self._ctx, float(epsilon), int(max_iterations)))
+
+    def status(self, first: int = 0, count: int = 0) -> Tuple[Status, List[Tuple[float, float]]]:
+        st = Status()
+        recs = (IterRecord * max(count, 1))()
+        check(self._lib.hmmbw_get_status(self._ctx, ctypes.byref(st), ctypes.cast(recs, ctypes.c_void_p) if count
+                                         else None, int(first), int(count)))
+        return st, [(recs[i].log_likelihood, recs[i].diff) for i in range(count)]
+
+    def enqueue_iterations(self, n: int, stats: Optional[torch.Tensor] = None, group=None) -> None:
+        """Enqueue n EM iterations (asynchronous).  Multi-rank when world_size > 1."""
+        if self.world_size == 1:
+            check(self._lib.hmmbw_iterate(self._ctx, int(n)))
+            return
+        import torch.distributed as dist
+        ptr = ctypes.c_void_p(stats.data_ptr())
+        for _ in range(int(n)):
+            check(self._lib.hmmbw_estep(self._ctx, ptr))
+            dist.all_reduce(stats, group=group)  # ONE RCCL all-reduce of the packed fp64 statistics
+            check(self._lib.hmmbw_mstep(self._ctx, ptr, self.n_seq_global))
+
+    def make_stats_buffer(self) -> torch.Tensor:
+        return torch.zeros(self.stats_len, dtype=torch.float64, device=f"cuda:{self.device}")
+
+    def train(self, epsilon: float = 1e-6, max_iterations: int = 100, on_iteration: Optional[IterCallback] = None,
+              group=None, max_chunk: int = 32) -> Status:
+        """Run EM to the reference's stop rule; on_iteration(k, L_k, diff_k) for every iteration."""
+        self.reset(epsilon, max_iterations)
+        stats = self.make_stats_buffer() if self.world_size > 1 else None
+        reported, chunk = 0, 1
+        while True:
+            st, _ = self.status()
+            if st.done:
+                break
+            n = max(1, min(chunk, int(max_iterations) - st.iterations))
+            self.enqueue_iterations(n, stats, group)
+            st, recs = self.status(reported, 0)
+            if on_iteration is not None and st.iterations > reported:
+                st, recs = self.status(reported, st.iterations - reported)
+                for k, (L, d) in enumerate(recs):
+                    on_iteration(reported + k, L, d)
+            reported = st.iterations
+            chunk = min(chunk * 2, max_chunk)
+            if st.done:
+                break
+        return st
+
+    # -------------------------------------------------------------------------------- results
+    def params(self, normalise: bool = True) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+        pi = np.zeros(self.N)
+        A = np.zeros((self.N, self.N))
+        B = np.zeros((self.N, self.M))
+        check(self._lib.hmmbw_get_params(self._ctx, pi.ctypes.data, A.ctypes.data, B.ctypes.data, int(normalise)))
+        return pi, A, B
+
+    def loglik(self) -> np.ndarray:
+        out = np.zeros(max(self.n_seq, 1))
+        check(self._lib.hmmbw_get_loglik(self._ctx, out.ctypes.data))
+        return out[: self.n_seq]
+
+    def score(self) -> np.ndarray:
+        """Forward-only log P(O_r | lambda) of every loaded sequence (hmm_testing.py:49-104)."""
+        out = np.zeros(max(self.n_seq, 1))
+        check(self._lib.hmmbw_score(self._ctx, out.ctypes.data))
+        return out[: self.n_seq]
+
+    def timing(self, enable: int = -1) -> Tuple[float, int]:
+        ms = ctypes.c_double()
+        n = ctypes.c_int64()
+        check(self._lib.hmmbw_timing(self._ctx, int(enable), ctypes.byref(ms), ctypes.byref(n)))
+        return ms.value, n.value
+
+    def close(self) -> None:
+        if getattr(self, "_ctx", None):
+            self._lib.hmmbw_ctx_destroy(self._ctx)
+            self._ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()

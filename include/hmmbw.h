@@ -1,0 +1,132 @@
+/*
+ * hmmbw.h — C ABI of the MI355X-native Baum-Welch engine (libhmmbw.so).
+ *
+ * The reference (DemianMArin/HMM_Training, pure Python/NumPy) has no FFI; its hot-path boundary is
+ * the Python function
+ *     hmm_training(observations, N=4, M=256, epsilon=1e-6, max_iterations=100,
+ *                  show_progress=True, word_name=None, load_initial_params=True) -> (A, B, pi)
+ * at HMM/hmm_training.py:265-267, its forward-only scorer
+ *     calculate_log_likelihood(recording_observations, hmm) -> float   (HMM/hmm_testing.py:49)
+ * and its VQ encoder get_observations (HMM/hmm_training.py:82-120).  Each entry point below says
+ * which part of those functions it replaces.  The Python drop-in (hmm_training_amd/) binds this
+ * ABI with ctypes; INTEGRATION.md shows the binding.
+ *
+ * Conventions
+ *  - Every function returns an int status: HMMBW_OK (0) or a negative HMMBW_E_* code; the message
+ *    of the last failure on the calling thread is hmmbw_last_error().  No C++ exception crosses
+ *    the ABI.
+ *  - All arrays are plain row-major host or device pointers with explicit sizes; no torch types.
+ *  - Probabilities are fp64, LINEAR domain (the reference converts with safe_log/safe_exp at
+ *    hmm_training.py:323-325 and :524-526; the engine's scaled-linear recursions are the same
+ *    quantities).
+ *  - Work is enqueued on the context's HIP stream (hmmbw_set_stream) and is asynchronous, except
+ *    the functions marked SYNC, which synchronise that stream.
+ *  - One context per device per thread; contexts are independent.
+ */
+#ifndef HMMBW_H
+#define HMMBW_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HMMBW_ABI_VERSION 1
+
+#define HMMBW_OK 0
+#define HMMBW_E_INVALID (-1)        /* bad argument (shape, range, null pointer)             */
+#define HMMBW_E_HIP (-2)            /* HIP runtime error                                      */
+#define HMMBW_E_UNSUPPORTED (-3)    /* shape outside what the kernels implement (N > 64)       */
+#define HMMBW_E_STATE (-4)          /* call order violated (e.g. estep before observations)   */
+#define HMMBW_E_EMPTY_SEQUENCE (-5) /* a sequence of length 0: the reference raises IndexError
+                                       at hmm_training.py:376 / hmm_testing.py:75              */
+#define HMMBW_E_SYMBOL_RANGE (-6)   /* symbol id >= M: numpy IndexError at hmm_training.py:360 */
+
+/* Transition-matrix kernel variant (the reference skips -inf transitions,
+ * hmm_training.py:143-144,186-188; a left-to-right A keeps its zero pattern under EM). */
+#define HMMBW_TOPOLOGY_AUTO 0          /* left-to-right if A's zero pattern allows, else dense */
+#define HMMBW_TOPOLOGY_DENSE 1
+#define HMMBW_TOPOLOGY_LEFT_TO_RIGHT 2 /* a_ij == 0 unless j in {i, i+1}                      */
+
+typedef struct hmmbw_ctx hmmbw_ctx;
+
+/* One EM iteration's convergence record: hmm_training.py:503-513 (L = LSE_r log P_r of the
+ * parameters ENTERING the iteration, diff = |L - L_prev| or +inf on the first iteration). */
+typedef struct {
+    double log_likelihood;
+    double diff;
+} hmmbw_iter_record;
+
+typedef struct {
+    int64_t iterations; /* EM iterations executed (the reference's `iteration`, :514)          */
+    int32_t done;       /* 1 once `diff >= epsilon and iteration < max_iterations` (:346) fails */
+    int32_t converged;  /* 1 if it stopped on epsilon rather than on max_iterations (:516-521)  */
+    double last_log_likelihood;
+    double last_diff;
+} hmmbw_status;
+
+int hmmbw_abi_version(void);
+const char *hmmbw_last_error(void);
+int hmmbw_device_count(int *out);
+
+/* Context for one (device, N states, M symbols) model.  Replaces the parameter set-up of
+ * hmm_training.py:268-339 (allocation is sized by hmmbw_set_observations). */
+int hmmbw_ctx_create(int device, int n_states, int n_symbols, hmmbw_ctx **out);
+int hmmbw_ctx_destroy(hmmbw_ctx *ctx);
+int hmmbw_set_stream(hmmbw_ctx *ctx, void *hip_stream); /* hipStream_t; NULL = legacy default */
+int hmmbw_set_rank(hmmbw_ctx *ctx, int rank, int world_size);
+int hmmbw_set_topology(hmmbw_ctx *ctx, int topology);
+int hmmbw_get_topology(const hmmbw_ctx *ctx, int *out); /* resolved variant (after AUTO)      */
+
+/* Observation sequences as host CSR: sequence r is symbols[offsets[r] .. offsets[r+1]).
+ * Replaces the `observations: List[np.ndarray]` argument (hmm_training.py:265) — the caller
+ * keeps ownership; the library copies to HBM in its own length-sorted, time-major layout. */
+int hmmbw_set_observations(hmmbw_ctx *ctx, const int64_t *offsets, const int32_t *symbols, int64_t n_seq);
+
+/* Linear (pi[N], A[N*N], B[N*M]) host arrays: the initial parameters (hmm_training.py:299-325). */
+int hmmbw_set_params(hmmbw_ctx *ctx, const double *pi, const double *A, const double *B);
+
+/* Arm a training run: epsilon and max_iterations of hmm_training.py:265-266,342-346. */
+int hmmbw_reset_training(hmmbw_ctx *ctx, double epsilon, int64_t max_iterations);
+
+/* Length (in doubles) of the packed sufficient-statistics buffer used by estep/mstep. */
+int hmmbw_stats_len(const hmmbw_ctx *ctx, int64_t *n_doubles);
+
+/* E-step over this rank's sequences (hmm_training.py:351-410): accumulates the packed statistics
+ * {pi_num[N], S[N*N], gamma_den_excl_last[N], gamma_den_all[N], B_num[M*N], (m, s)[world]}
+ * into the zero-filled DEVICE buffer stats_dev and writes this rank's (max, sum-exp) pair of
+ * log P_r into its slot.  Multi-rank callers all-reduce(sum) stats_dev, then call hmmbw_mstep. */
+int hmmbw_estep(hmmbw_ctx *ctx, double *stats_dev);
+
+/* M-step + convergence (hmm_training.py:415-514) from the (all-reduced) statistics; n_seq_global
+ * is the R of :424.  Zero-fills stats_dev for the next iteration.  No-op once done. */
+int hmmbw_mstep(hmmbw_ctx *ctx, double *stats_dev, int64_t n_seq_global);
+
+/* Single-rank fused loop: enqueue n_iter iterations of (estep, mstep) with internal statistics.
+ * Iterations after convergence are device-side no-ops (same result as stopping, :346). */
+int hmmbw_iterate(hmmbw_ctx *ctx, int64_t n_iter);
+
+/* SYNC. Status plus the iteration records [first, first+count) (ring of 4096 entries). */
+int hmmbw_get_status(hmmbw_ctx *ctx, hmmbw_status *status, hmmbw_iter_record *records, int64_t first,
+                     int64_t count);
+
+/* SYNC. Current parameters.  normalise=1 applies the reference's return path (safe_exp then
+ * pi/sum(pi), row-normalise A and B rows with positive sums, :524-541); normalise=0 returns the
+ * unnormalised working parameters (exp of the reference's log_pi/log_a/log_b matrices). */
+int hmmbw_get_params(hmmbw_ctx *ctx, double *pi, double *A, double *B, int normalise);
+
+/* SYNC. log P(O_r | lambda) of the last E-step, in the caller's sequence order (:375-377). */
+int hmmbw_get_loglik(hmmbw_ctx *ctx, double *out);
+
+/* SYNC. Forward-only scoring of the loaded sequences under the current parameters:
+ * hmm_testing.py:49-104 calculate_log_likelihood for every sequence, one launch. */
+int hmmbw_score(hmmbw_ctx *ctx, double *out);
+
+/* E-step kernel timing with HIP events on the context stream (for bench/roofline). */
+int hmmbw_timing(hmmbw_ctx *ctx, int enable, double *total_ms, int64_t *count);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HMMBW_H */

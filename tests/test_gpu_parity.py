@@ -1,0 +1,268 @@
+"""GPU parity: the HIP engine (through the C ABI) against the reference's golden vectors and the
+oracle restatement.  Run on an MI355X with `pytest -m gpu`.
+
+Tolerance (north_star: "within 1e-6 relative"): parameters |x - ref| <= 1e-6 * |ref| + 1e-15.  The
+absolute 1e-15 term covers entries the reference's safe_exp underflows to exactly 0.0
+or leaves at ~1e-300, which the scaled-linear fp64 engine holds as ~1e-300 or at the 1e-20 floor.
+Log-likelihoods: relative 1e-9.
+"""
+import contextlib
+import io
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, ROOT, golden_cases
+
+pytestmark = pytest.mark.gpu
+
+PARAM_RTOL, PARAM_ATOL, LL_RTOL = 1e-6, 1e-15, 1e-9
+
+
+@pytest.fixture(scope="module", autouse=True)
+def gpu():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.fail("no HIP device visible: the GPU tests need an MI355X")
+    from hmm_training_amd import _lib
+    _lib.lib()
+
+
+def load(case):
+    return np.load(f"{GOLDEN}/bw_{case}.npz", allow_pickle=False)
+
+
+def observations(d):
+    off, sym = d["offsets"], d["symbols"]
+    return [sym[off[i]:off[i + 1]] for i in range(len(off) - 1)]
+
+
+def assert_params(mine, ref, what):
+    mine, ref = np.asarray(mine), np.asarray(ref)
+    err = np.abs(mine - ref) - (PARAM_RTOL * np.abs(ref) + PARAM_ATOL)
+    assert np.all(err <= 0), f"{what}: worst excess {err.max():.3e} at {np.unravel_index(np.argmax(err), err.shape)}"
+
+
+def assert_ll(mine, ref, rtol=LL_RTOL):
+    mine, ref = np.asarray(mine, dtype=float), np.asarray(ref, dtype=float)
+    assert np.array_equal(np.isneginf(mine), np.isneginf(ref))
+    f = np.isfinite(ref)
+    np.testing.assert_allclose(mine[f], ref[f], rtol=rtol)
+
+
+def run_dropin(d, tmp_path, monkeypatch, **kw):
+    """Call the drop-in hmm_training exactly as the reference was called for this fixture."""
+    from hmm_training_amd.hmm_classes import DataStorageHMM, HMMTrained
+    from hmm_training_amd.hmm_training import hmm_training
+    N, M = int(d["N"]), int(d["M"])
+    warm = bool(d["load_initial"])
+    os.makedirs(tmp_path / "cwd", exist_ok=True)
+    if warm:
+        DataStorageHMM.save_hmm(HMMTrained(N, M, d["init_A"], d["init_B"], d["init_pi"], "w"),
+                                base_dir=str(tmp_path / "Data" / "Eighty-five-percent_20"), print_messages=False)
+    monkeypatch.chdir(tmp_path / "cwd")
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        A, B, pi = hmm_training(observations(d), N=N, M=M, epsilon=float(d["epsilon"]),
+                                max_iterations=int(d["max_iterations"]), show_progress=True,
+                                word_name="w" if warm else None, load_initial_params=warm, **kw)
+    return A, B, pi, buf.getvalue().splitlines()
+
+
+@pytest.mark.parametrize("case", golden_cases())
+def test_dropin_matches_reference(case, tmp_path, monkeypatch):
+    d = load(case)
+    A, B, pi, lines = run_dropin(d, tmp_path, monkeypatch)
+    assert_params(A, d["out_A"], "A")
+    assert_params(B, d["out_B"], "B")
+    assert_params(pi, d["out_pi"], "pi")
+    assert lines == list(d["stdout"]), "printed progress differs from the reference"
+
+
+@pytest.mark.parametrize("topology", ["auto", "dense"])
+@pytest.mark.parametrize("case", golden_cases())
+def test_engine_internals_match_reference(case, topology):
+    from hmm_training_amd.engine import BaumWelchEngine
+    d = load(case)
+    N, M = int(d["N"]), int(d["M"])
+    with BaumWelchEngine(N, M, topology=topology) as eng:
+        eng.set_observations(observations(d))
+        eng.set_params(d["init_pi"], d["init_A"], d["init_B"])
+        trace = []
+        st = eng.train(float(d["epsilon"]), int(d["max_iterations"]), lambda k, L, df: trace.append((L, df)))
+        assert st.iterations == int(d["iterations"])
+        assert_ll([t[0] for t in trace], d["trace_L"])
+        assert_ll(eng.loglik(), d["trace_logP"][-1])
+        pi, A, B = eng.params(normalise=False)
+        with np.errstate(under="ignore"):
+            assert_params(pi, np.exp(d["trace_log_pi"][-1]), "log_pi")
+            assert_params(A, np.exp(d["trace_log_A"][-1]), "log_A")
+            assert_params(B, np.exp(d["trace_log_B"][-1]), "log_B")
+        # forward-only scorer (hmm_testing.py:49-104) under the returned model
+        eng.set_params(d["out_pi"], d["out_A"], d["out_B"])
+        assert_ll(eng.score(), d["score_loglik"])
+
+
+def random_problem(rng, N, K, R, tmax, topology):
+    lengths = rng.integers(1, tmax + 1, size=R)
+    lengths[0] = tmax
+    obs = [rng.integers(0, K, size=int(t)) for t in lengths]
+    if topology == "left_to_right":
+        A = np.zeros((N, N))
+        for i in range(N):
+            A[i, i] = rng.uniform(0.3, 0.9)
+            if i + 1 < N:
+                A[i, i + 1] = 1 - A[i, i]
+            else:
+                A[i, i] = 1.0
+        pi = np.zeros(N)
+        pi[0] = 0.8
+        pi[1:] = 0.2 / max(N - 1, 1)
+        if N == 1:
+            pi[0] = 1.0
+    else:
+        A = rng.dirichlet(np.ones(N), size=N)
+        pi = rng.dirichlet(np.ones(N))
+    B = rng.dirichlet(np.full(K, 0.5), size=N)
+    return obs, pi, A, B
+
+
+SWEEP = [(N, K, topo) for N in (1, 2, 3, 4, 5, 7, 8, 9, 12, 16) for K, topo in ((16, "dense"), (256, "left_to_right"))]
+SWEEP += [(8, 700, "dense"), (8, 700, "left_to_right"), (16, 300, "dense"), (17, 40, "dense"), (24, 128, "dense"),
+          (33, 64, "dense"), (64, 300, "dense")]
+
+
+@pytest.mark.parametrize("N,K,topology", SWEEP)
+def test_training_vs_oracle_random(N, K, topology, oracle):
+    from hmm_training_amd.engine import BaumWelchEngine, to_csr
+    rng = np.random.default_rng(1000 * N + K)
+    obs, pi, A, B = random_problem(rng, N, K, R=37, tmax=90, topology=topology)
+    off, sym = to_csr(obs)
+    ref = oracle.hmm_training(off, sym.astype(np.int64), N, K, 1e-6, 3, pi, A, B)
+    with BaumWelchEngine(N, K, topology=topology) as eng:
+        eng.set_observations(obs)
+        eng.set_params(pi, A, B)
+        assert eng.topology == topology
+        trace = []
+        eng.train(1e-6, 3, lambda k, L, df: trace.append(L))
+        assert_ll(trace, ref.trace_L)
+        assert_ll(eng.loglik(), ref.logP)
+        p2, A2, B2 = eng.params(normalise=True)
+    assert_params(A2, ref.A, "A")
+    assert_params(B2, ref.B, "B")
+    assert_params(p2, ref.pi, "pi")
+
+
+@pytest.mark.parametrize("topology", ["dense", "left_to_right"])
+def test_estep_statistics_vs_oracle(topology, oracle):
+    import torch
+    from hmm_training_amd.engine import BaumWelchEngine, StatsLayout, to_csr
+    rng = np.random.default_rng(7)
+    N, K = 8, 256
+    obs, pi, A, B = random_problem(rng, N, K, R=200, tmax=160, topology=topology)
+    off, sym = to_csr(obs)
+    s = oracle.estep_logstats(off, sym.astype(np.int64), N, K, pi, A, B)
+    with BaumWelchEngine(N, K, topology=topology) as eng:
+        eng.set_observations(obs)
+        eng.set_params(pi, A, B)
+        eng.reset(1e-6, 10)
+        stats = eng.make_stats_buffer()
+        from hmm_training_amd._lib import check
+        import ctypes
+        check(eng._lib.hmmbw_estep(eng._ctx, ctypes.c_void_p(stats.data_ptr())))
+        torch.cuda.synchronize()
+        got = StatsLayout(N, K).decode(stats.cpu().numpy())
+        assert_ll(eng.loglik(), s.logP)
+    np.testing.assert_allclose(got["pi_num"], np.exp(s.log_pi_num), rtol=1e-9, atol=1e-300)
+    np.testing.assert_allclose(A * got["S"], np.exp(s.log_xi), rtol=1e-9, atol=1e-300)
+    np.testing.assert_allclose(got["gamma_den_excl"], np.exp(s.log_gden_excl), rtol=1e-9)
+    np.testing.assert_allclose(got["gamma_den_all"], np.exp(s.log_gden_all), rtol=1e-9)
+    np.testing.assert_allclose(got["B_num"], np.exp(s.log_bnum), rtol=1e-9, atol=1e-300)
+    lp = s.logP[np.isfinite(s.logP)]
+    assert np.isclose(StatsLayout.lse_of_pairs(got["ll_pairs"]), oracle.lse(lp), rtol=1e-12)
+
+
+def test_full_size_cfg3_properties(oracle):
+    """BASELINE cfg3 size (R=10,000, T=200, N=8, K=256): size-independent properties of one E-step
+    plus oracle parity on a sample of sequences."""
+    import ctypes
+    import torch
+    from hmm_training_amd._lib import check
+    from hmm_training_amd.engine import BaumWelchEngine, StatsLayout
+    from hmm_training_amd.hmm_training import default_initial_params
+    rng = np.random.default_rng(3)
+    R, T, N, K = 10_000, 200, 8, 256
+    sym = rng.integers(0, K, size=(R, T))
+    pi, A, B = default_initial_params(N, K)
+    B = rng.dirichlet(np.full(K, 2.0), size=N)
+    with BaumWelchEngine(N, K) as eng:
+        assert eng.topology == "left_to_right"
+        eng.set_observations(offsets=np.arange(R + 1) * T, symbols=sym.reshape(-1))
+        eng.set_params(pi, A, B)
+        eng.reset(0.0, 1)
+        stats = eng.make_stats_buffer()
+        check(eng._lib.hmmbw_estep(eng._ctx, ctypes.c_void_p(stats.data_ptr())))
+        torch.cuda.synchronize()
+        g = StatsLayout(N, K).decode(stats.cpu().numpy())
+        ll = eng.loglik()
+    assert np.all(np.isfinite(ll))
+    np.testing.assert_allclose(g["B_num"].sum(1), g["gamma_den_all"], rtol=1e-11)
+    np.testing.assert_allclose((A * g["S"]).sum(1), g["gamma_den_excl"], rtol=1e-11)
+    assert np.isclose(g["pi_num"].sum(), R, rtol=1e-12)
+    assert np.isclose(g["gamma_den_all"].sum(), R * T, rtol=1e-12)
+    pick = rng.choice(R, size=48, replace=False)
+    ref = oracle.forward_loglik(np.arange(len(pick) + 1) * T, sym[pick].reshape(-1).astype(np.int64), N, K, pi, A, B)
+    np.testing.assert_allclose(ll[pick], ref, rtol=1e-11)
+    assert np.isclose(StatsLayout.lse_of_pairs(g["ll_pairs"]), oracle.lse(ll), rtol=1e-12)
+
+
+def test_converged_iterations_are_noops():
+    from hmm_training_amd.engine import BaumWelchEngine
+    d = load("converge")
+    N, M = int(d["N"]), int(d["M"])
+    with BaumWelchEngine(N, M) as eng:
+        eng.set_observations(observations(d))
+        eng.set_params(d["init_pi"], d["init_A"], d["init_B"])
+        st = eng.train(1e-6, 100)
+        assert st.done and st.converged and st.iterations == int(d["iterations"])
+        before = eng.params(normalise=False)
+        eng.enqueue_iterations(5)
+        st2, _ = eng.status()
+        assert st2.iterations == st.iterations
+        after = eng.params(normalise=False)
+    for x, y in zip(before, after):
+        np.testing.assert_array_equal(x, y)
+
+
+def test_error_behaviour():
+    from hmm_training_amd.hmm_training import hmm_training
+    with pytest.raises(IndexError):
+        hmm_training([np.array([1, 2]), np.array([], dtype=np.int64)], N=4, M=8, show_progress=False,
+                     load_initial_params=False)
+    with pytest.raises(IndexError):
+        hmm_training([np.array([1, 9])], N=4, M=8, show_progress=False, load_initial_params=False)
+    with pytest.raises(UnboundLocalError):
+        hmm_training([np.array([1, 2])], N=4, M=8, max_iterations=0, show_progress=False,
+                     load_initial_params=False)
+
+
+def test_score_matrix_and_timing():
+    from hmm_training_amd.engine import BaumWelchEngine
+    from hmm_training_amd.hmm_classes import HMMTrained
+    from hmm_training_amd.hmm_testing import calculate_log_likelihood, score_matrix
+    d = load("n8_k256_cfg2")
+    obs = observations(d)
+    m = HMMTrained(8, 256, d["out_A"], d["out_B"], d["out_pi"], "w")
+    S = score_matrix(obs, [m, m])
+    assert_ll(S[:, 0], d["score_loglik"])
+    assert_ll(S[:, 1], d["score_loglik"])
+    assert np.isclose(calculate_log_likelihood(obs[0], m), d["score_loglik"][0], rtol=LL_RTOL)
+    with BaumWelchEngine(8, 256) as eng:
+        eng.set_observations(obs)
+        eng.set_params(d["init_pi"], d["init_A"], d["init_B"])
+        eng.timing(1)
+        eng.reset(0.0, 4)
+        eng.enqueue_iterations(4)
+        ms, n = eng.timing(0)
+        assert n == 4 and ms > 0

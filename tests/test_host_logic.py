@@ -1,0 +1,122 @@
+"""CPU tests of the host-side logic: library exports, model surface / JSON schema, default init,
+CSR packing, sharding, the reference helper functions."""
+import ctypes
+import json
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, ROOT
+
+
+def header_functions():
+    text = open(os.path.join(ROOT, "include", "hmmbw.h")).read()
+    return sorted(set(re.findall(r"^\s*(?:int|const char \*)\s*(hmmbw_\w+)\s*\(", text, flags=re.M)))
+
+
+def test_library_exports_every_header_symbol():
+    from hmm_training_amd import _lib
+    lib = _lib.lib()
+    declared = header_functions()
+    assert set(declared) == set(_lib.EXPORTED), "binding table out of sync with include/hmmbw.h"
+    for name in declared:
+        assert hasattr(lib, name), name
+    assert lib.hmmbw_abi_version() == 1
+
+
+def test_library_fails_loudly_without_device_or_bad_args():
+    from hmm_training_amd import _lib
+    lib = _lib.lib()
+    ctx = ctypes.c_void_p()
+    assert lib.hmmbw_ctx_create(0, 0, 4, ctypes.byref(ctx)) == _lib.HMMBW_E_INVALID
+    assert lib.hmmbw_ctx_create(0, 65, 4, ctypes.byref(ctx)) == _lib.HMMBW_E_UNSUPPORTED
+    with pytest.raises(ValueError):
+        _lib.check(_lib.HMMBW_E_INVALID)
+    with pytest.raises(IndexError):
+        _lib.check(_lib.HMMBW_E_EMPTY_SEQUENCE)
+
+
+def test_missing_library_raises(monkeypatch, tmp_path):
+    import importlib
+    from hmm_training_amd import _lib
+    monkeypatch.setattr(_lib, "_lib", None)
+    monkeypatch.setattr(_lib, "LIB_PATH", str(tmp_path / "nope.so"))
+    with pytest.raises(ImportError):
+        _lib.lib()
+
+
+def test_json_schema_byte_compatible(tmp_path):
+    from hmm_training_amd.hmm_classes import DataStorageHMM, HMMTrained
+    ref_text = open(os.path.join(GOLDEN, "hmm_json_schema.json")).read()
+    d = json.loads(ref_text)
+    m = HMMTrained.from_dict(d)
+    DataStorageHMM.save_hmm(m, base_dir=str(tmp_path), print_messages=False)
+    assert open(tmp_path / "golden.json").read() == ref_text
+    again = DataStorageHMM.load_hmm("golden", str(tmp_path), print_messages=False)
+    np.testing.assert_array_equal(again.B, m.B)
+    (tmp_path / "broken.json").write_text("{")
+    models = DataStorageHMM.load_all_hmms(str(tmp_path), print_messages=False)
+    assert [x.word for x in models] == ["golden"]
+
+
+def test_default_init_matches_reference_for_n4():
+    from hmm_training_amd.hmm_training import default_initial_params
+    d = np.load(os.path.join(GOLDEN, "bw_n4_k16_default.npz"), allow_pickle=False)
+    pi, A, B = default_initial_params(4, 16)
+    np.testing.assert_array_equal(pi, d["init_pi"])
+    np.testing.assert_array_equal(A, d["init_A"])
+    np.testing.assert_array_equal(B, d["init_B"])
+    pi8, A8, B8 = default_initial_params(8, 256)
+    np.testing.assert_allclose(A8.sum(1), 1.0)
+    assert pi8[0] == 0.97 and np.isclose(pi8.sum(), 1.0)
+    pi3, A3, _ = default_initial_params(3, 5)  # the reference reads the leading block of its 4-state arrays
+    np.testing.assert_array_equal(pi3, [0.97, 0.02, 0.005])
+    np.testing.assert_array_equal(A3[2], [0.0, 0.0, 0.6])
+
+
+def test_reference_helpers():
+    from hmm_training_amd.hmm_training import log_sum_exp, safe_exp, safe_log
+    x = np.array([0.0, 1.0, -2.0, 0.5])
+    np.testing.assert_array_equal(safe_log(x)[[0, 2]], [-np.inf, -np.inf])
+    assert safe_log(0.0) == -np.inf and safe_exp(-np.inf) == 0.0
+    assert log_sum_exp(np.array([-np.inf, -np.inf])) == -np.inf
+    assert np.isclose(log_sum_exp(np.log(np.array([1.0, 2.0, 0.0]))), np.log(3.0))
+    assert log_sum_exp(-3.0) == -3.0
+
+
+def test_csr_and_shards():
+    from hmm_training_amd.engine import shard_bounds, to_csr
+    obs = [np.arange(5), np.arange(1), np.arange(7) % 3]
+    off, sym = to_csr(obs)
+    assert off.tolist() == [0, 5, 6, 13] and sym.dtype == np.int32
+    rng = np.random.default_rng(0)
+    lengths = rng.integers(1, 300, size=1001)
+    for world in (1, 2, 3, 4, 8):
+        b = shard_bounds(lengths, world)
+        assert b[0][0] == 0 and b[-1][1] == len(lengths)
+        assert all(b[i][1] == b[i + 1][0] for i in range(world - 1))
+        loads = [lengths[s:e].sum() for s, e in b]
+        assert max(loads) - min(loads) <= 2 * lengths.max()
+
+
+def test_get_observations_matches_reference_vq():
+    from types import SimpleNamespace as NS
+    from hmm_training_amd.hmm_training import get_observations
+    d = np.load(os.path.join(GOLDEN, "vq_k64.npz"), allow_pickle=False)
+    off = d["offsets"]
+    recs = [[NS(mfcc=f) for f in d["frames"][off[i]:off[i + 1]]] for i in range(len(off) - 1)]
+    out = get_observations(recs, [NS(mfcc=c) for c in d["centroids"]])
+    assert np.array_equal(np.concatenate(out), d["symbols"])
+
+
+def test_stats_layout_roundtrip():
+    from hmm_training_amd.engine import StatsLayout
+    L = StatsLayout(3, 5, world=2)
+    assert L.length == 3 + 9 + 3 + 3 + 15 + 4
+    buf = np.arange(L.length, dtype=np.float64)
+    d = L.decode(buf)
+    assert d["B_num"].shape == (3, 5) and d["B_num"][1, 0] == L.bnum + 1
+    assert np.isclose(StatsLayout.lse_of_pairs([[-3.0, 1.0], [0.0, 0.0]]), -3.0)
+    assert StatsLayout.lse_of_pairs([[0.0, 0.0]]) == -np.inf
