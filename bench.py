@@ -67,7 +67,7 @@ def bytes_per_sequence(T, N):
 def find_traffic(cfg_key):
     """Per-launch HBM bytes of the E-step kernel from a committed PMC summary for this config."""
     best = None
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*traffic*.json"))):
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "**", "*traffic*.json"), recursive=True)):
         try:
             with open(path) as fh:
                 d = json.load(fh)
@@ -93,7 +93,7 @@ def cpu_baseline(N, K, T, topology, budget_s, seed):
 
     probe_R = 8
     dt = run(probe_R)
-    R = int(max(probe_R, min(4096, probe_R * budget_s / max(dt, 1e-6))))
+    R = int(max(probe_R, min(200_000, probe_R * budget_s / max(dt, 1e-6))))
     dt = run(R)
     return {"value": R / dt, "unit": "utterances/s/iter", "cores": 1, "kind": "port",
             "sample": f"{R} sequences x 1 EM iteration (T={T}, N={N}, K={K}, {topology}) on the oracle "

@@ -197,9 +197,9 @@ def test_full_size_cfg3_properties(oracle):
     pi, A, B = default_initial_params(N, K)
     B = rng.dirichlet(np.full(K, 2.0), size=N)
     with BaumWelchEngine(N, K) as eng:
-        assert eng.topology == "left_to_right"
         eng.set_observations(offsets=np.arange(R + 1) * T, symbols=sym.reshape(-1))
         eng.set_params(pi, A, B)
+        assert eng.topology == "left_to_right"
         eng.reset(0.0, 1)
         stats = eng.make_stats_buffer()
         check(eng._lib.hmmbw_estep(eng._ctx, ctypes.c_void_p(stats.data_ptr())))
