@@ -23,7 +23,8 @@
 //        backward sweep, which fuses beta, gamma, xi and the histogram scatter.
 //   k_estep_wide<NP,FWD_ONLY>              16 < N <= 64: one sequence per wavefront, lane = state,
 //        A / A^T in LDS, alpha / v exchanged through a per-wave LDS row.
-//   k_seq_lse   per-rank (max, sum exp) pair of log P_r into the rank's statistics slot.
+//   k_reduce_local  (multi-rank) sum the statistics copies into the all-reduce buffer + the rank's
+//                   (max, sum exp) pair of log P_r.
 //   k_mstep     one workgroup: L, M-step, convergence record, zero the statistics.
 //   k_finalise  the reference's return-path normalisation (:524-541).
 #include <hip/hip_runtime.h>
@@ -44,6 +45,7 @@ namespace hmmbw {
 
 constexpr int kWave = 64;
 constexpr int kChunk = 8;  // time steps per packed symbol load (8 x uint16 = 16 B)
+constexpr int kScale = 4;  // lagged mode: the forward rescales every kScale steps
 constexpr int kHist = 4096;
 constexpr int kBlock = 256;  // threads per E-step workgroup (4 waves)
 
@@ -60,14 +62,17 @@ struct IterState {
 
 // Observation layout in HBM (built once by hmmbw_set_observations).
 //   slot = wave * U + u  ->  caller sequence slot_seq[slot] (-1: padding), length slot_len[slot]
-//   symbols: per wave, chunk-major [chunk][u][8] uint16  (one 16-B load = 8 steps of one sequence)
-//   alpha_hat: per wave [t][64 lanes] fp64 ; exponents: per wave [t][u] int32 (+1 chunk pad)
+//   sym    : per wave, chunk-major [chunk][u][8] uint16  (one 16-B load = 8 steps of one sequence)
+//   ckpt   : per wave [chunk][64 lanes] fp64 — alpha_hat at the first step of every chunk (small N)
+//   spack  : per wave [chunk][u] 8 x int16 — the power-of-two scale exponent of every step
+//   alpha  : per wave [t][64 lanes] fp64 + ebuf [t][u] int32 — full alpha_hat (wide kernel only)
 struct Layout {
     const uint16_t *sym;
     const long long *wave_symoff;
-    const long long *wave_aoff;
-    const long long *wave_eoff;
+    const long long *wave_ckoff;   // doubles (small) | alpha doubles (wide)
+    const long long *wave_spoff;   // uint4 units (small) | ebuf ints (wide)
     const int *wave_T;
+    const int *wave_full;          // 1: every real slot of the wave has length wave_T
     const int *slot_len;
     const int *slot_seq;
     long long nwaves;
@@ -77,14 +82,20 @@ struct EArgs {
     Layout L;
     const double *pi;
     const double *A;
-    const double *Bt;  // [K][G]
-    double *alpha;
-    int *ebuf;
-    double *stats;
+    const double *Bt;  // [K][G] + G zero pad
+    double *ckpt;      // small: checkpoints | wide: alpha_hat
+    uint4 *spack;      // small: scale exponents
+    int *ebuf;         // wide: scale exponents
+    double *copies;    // [ncopies][copy_len] statistics accumulators (workgroup b adds into copy b % ncopies)
+    long long copy_len;
+    int ncopies;
     double *logp;
+    double *llpart;    // [blocks][2]: per-block (max, sum exp) of log P
     const IterState *state;
     int K;
     int N;
+    int force_safe;    // 1: per-step normalisation (no lagged scaling)
+    int ablate;        // diagnostics only: bit 0 skips the statistics flush, bit 1 the backward sweep
     long long off_S, off_gex, off_gall, off_bnum;
 };
 
@@ -98,6 +109,11 @@ __device__ __forceinline__ double dpp(double v) {
     return __builtin_bit_cast(double, x);
 }
 
+template <int CTRL>
+__device__ __forceinline__ int dpp_i32(int v) {
+    return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, true);
+}
+
 // Sum over a group of G lanes (butterfly; every lane gets the bitwise-identical result because
 // each level adds the same two partial sums, only commuted).
 template <int G>
@@ -109,6 +125,23 @@ __device__ __forceinline__ double gsum(double x) {
     if constexpr (G >= 32) x += __shfl_xor(x, 16);
     if constexpr (G >= 64) x += __shfl_xor(x, 32);
     return x;
+}
+
+template <int G>
+__device__ __forceinline__ int gmax_i32(int e) {
+    if constexpr (G >= 2) e = max(e, dpp_i32<0xB1>(e));
+    if constexpr (G >= 4) e = max(e, dpp_i32<0x4E>(e));
+    if constexpr (G >= 8) e = max(e, dpp_i32<0x141>(e));
+    if constexpr (G >= 16) e = max(e, dpp_i32<0x140>(e));
+    return e;
+}
+
+// Exponent that steers the power-of-two scaling: frexp exponent of the group's largest entry
+// (entries are >= 0), kZeroExp when the whole group is zero.
+constexpr int kZeroExp = -8192;
+template <int G>
+__device__ __forceinline__ int group_exp(double z) {
+    return gmax_i32<G>(z > 0.0 ? __builtin_amdgcn_frexp_exp(z) : kZeroExp);
 }
 
 // Value of lane I of this lane's G-group.
@@ -141,52 +174,111 @@ __device__ __forceinline__ int sym_of(const uint4 &p, int s) {
     return (s & 1) ? int(w >> 16) : int(w & 0xFFFFu);
 }
 
+__device__ __forceinline__ int exp_of(const uint4 &p, int s) {  // signed int16 lanes of a pack
+    const unsigned w = s < 2 ? p.x : (s < 4 ? p.y : (s < 6 ? p.z : p.w));
+    return (s & 1) ? int((int)w >> 16) : int((int)(w << 16) >> 16);
+}
+
+__device__ __forceinline__ uint4 pack_exps(const int *e) {
+    uint4 p;
+    p.x = (unsigned)(e[0] & 0xFFFF) | ((unsigned)e[1] << 16);
+    p.y = (unsigned)(e[2] & 0xFFFF) | ((unsigned)e[3] << 16);
+    p.z = (unsigned)(e[4] & 0xFFFF) | ((unsigned)e[5] << 16);
+    p.w = (unsigned)(e[6] & 0xFFFF) | ((unsigned)e[7] << 16);
+    return p;
+}
+
 __device__ __forceinline__ double pow2_scale(double x, int e) { return __builtin_amdgcn_ldexp(x, -e); }
 
+// Per-block (max, sum exp(x - max)) of the sequences' log P (each sequence contributes from
+// exactly one lane with valid = true).  All threads of the block call it.
+__device__ void block_ll_partial(double lp, bool valid, double *sh, double *out) {
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, nw = blockDim.x >> 6;
+    double m = valid ? lp : -INFINITY;
+    for (int k = 32; k >= 1; k >>= 1) m = fmax(m, __shfl_xor(m, k));
+    if (lane == 0) sh[wv] = m;
+    __syncthreads();
+    double M = -INFINITY;
+    for (int w = 0; w < nw; ++w) M = fmax(M, sh[w]);
+    double s = (valid && M != -INFINITY && lp != -INFINITY) ? exp(lp - M) : 0.0;
+    for (int k = 32; k >= 1; k >>= 1) s += __shfl_xor(s, k);
+    __syncthreads();
+    if (lane == 0) sh[wv] = s;
+    __syncthreads();
+    if (tid == 0) {
+        double S = 0.0;
+        for (int w = 0; w < nw; ++w) S += sh[w];
+        out[0] = (S > 0.0) ? M : 0.0;
+        out[1] = S;
+    }
+}
+
 // ---------------------------------------------------------------------------------------------
-// Small-N E-step / scorer.  One G-lane group per sequence.
+// Small-N E-step / scorer.  One G-lane group per sequence (lane j = state j), 64/G per wave.
+//
+// Forward: z_t = alpha_t / 2^{C_t}, C_t = s_0 + ... + s_t.  In the default (lagged) mode the scale
+// exponent applied at step t is chosen two steps early, s_t = M_{t-2} - s_{t-1} with M = the group's
+// largest frexp exponent, so that C_t tracks log2 of alpha_{t-2}'s magnitude and the per-step
+// dependency chain is just (DPP shift || multiply) -> fma; the scaling itself is folded into the
+// emission factor b_j(o_t) * 2^{-s_t} (exact).  If a wave's magnitudes ever leave [2^-900, 2^900]
+// (pathological parameters) the wave re-runs its forward in the safe mode, which normalises every
+// step by its own group maximum.  Only z at the first step of every 8-step chunk (the checkpoint)
+// and the s_t are stored; the backward sweep recomputes each chunk's z_t in registers with the
+// identical instruction sequence (bit-identical), so alpha never round-trips through HBM.
+//
+// Backward (Rabiner scaling with c_t = 2^{s_t}): beta_hat_{T-1} = 1/phat, phat = sum_j z_{T-1}(j);
+//   v_j = b_j(o_{t+1}) 2^{-s_{t+1}} beta_hat_{t+1}(j),  beta_hat_t(i) = sum_j a_ij v_j,
+//   gamma_t(i) = z_t(i) beta_hat_t(i),  xi_t(i,j) = a_ij z_t(i) v_j  (accumulated as S_ij = xi/a_ij).
+// gamma is scattered into the per-workgroup LDS histogram B_num[o_t][j] (ds_add_f64).
 // ---------------------------------------------------------------------------------------------
 template <int N, int G, bool LR, bool LDSTAB, bool FWD_ONLY>
 __global__ void __launch_bounds__(kBlock) k_estep_small(EArgs a) {
     constexpr int U = kWave / G;
     constexpr int NS = LR ? 2 : N;      // per-lane S accumulators (row j of S)
     constexpr int NV = NS + 3;          // + gamma_den_excl, gamma_den_all, pi_num
+    constexpr int GP = LDSTAB ? G + 1 : G;  // row stride of the emission / histogram tables
     extern __shared__ double smem[];
     if (a.state != nullptr && a.state->done) return;  // converged: device-side no-op
 
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int j = lane & (G - 1), u = lane / G;
     const int K = a.K;
-    double *sBt = smem;                                  // [K][G]
-    double *sBn = LDSTAB ? smem + (size_t)K * G : nullptr; // [K][G]
-    double *sRed = smem + (LDSTAB ? 2 : 0) * (size_t)K * G; // [waves][G][NV]
+    double *sBt = smem;                                               // [K][GP] + pad
+    double *sBn = smem + (LDSTAB ? (size_t)K * GP + GP : 0);          // [K][GP]
+    double *sRed = sBn + ((LDSTAB && !FWD_ONLY) ? (size_t)K * GP : 0); // [waves][G][NV] + ll scratch
     if constexpr (LDSTAB) {
-        for (int i = tid; i < K * G; i += blockDim.x) {
-            sBt[i] = a.Bt[i];
-            if constexpr (!FWD_ONLY) sBn[i] = 0.0;
+        for (int i = tid; i < (K + 1) * GP; i += blockDim.x) {
+            const int k = i / GP, c = i - k * GP;
+            sBt[i] = (k < K && c < G) ? a.Bt[(size_t)k * G + c] : 0.0;
+            if constexpr (!FWD_ONLY)
+                if (k < K) sBn[i] = 0.0;
         }
     }
     __syncthreads();
     const double *Btab = LDSTAB ? sBt : a.Bt;
 
     const long long wave = (long long)blockIdx.x * (blockDim.x >> 6) + wv;
+    double *accb = a.copies + (long long)(blockIdx.x % a.ncopies) * a.copy_len;
     double S[NS];
 #pragma unroll
     for (int k = 0; k < NS; ++k) S[k] = 0.0;
     double gex = 0.0, gall = 0.0, pin = 0.0;
+    double logp_lane = -INFINITY;
+    bool ll_valid = false;
 
     if (wave < a.L.nwaves) {
         const long long slot = wave * U + u;
         const int T = a.L.slot_len[slot];
         const int seq = a.L.slot_seq[slot];
         const int Tw = a.L.wave_T[wave];
+        const bool full = a.L.wave_full[wave] != 0;
         const int nch = (Tw + kChunk - 1) / kChunk;
         const uint16_t *symw = a.L.sym + a.L.wave_symoff[wave] + u * kChunk;
-        double *aw = a.alpha + (FWD_ONLY ? 0 : a.L.wave_aoff[wave]) + lane;
-        int *ew = a.ebuf + (FWD_ONLY ? 0 : a.L.wave_eoff[wave]) + u;
+        double *ckw = a.ckpt + (FWD_ONLY ? 0 : a.L.wave_ckoff[wave]) + lane;
+        uint4 *spw = a.spack + (FWD_ONLY ? 0 : a.L.wave_spoff[wave]) + u;
         const bool jv = j < N;
 
-        // transition coefficients for this lane (state j)
+        // transition coefficients of this lane (state j)
         double acol[LR ? 1 : N], arow[LR ? 1 : N];
         double a_dg = 0.0, a_in = 0.0, a_up = 0.0;
         if constexpr (LR) {
@@ -205,139 +297,259 @@ __global__ void __launch_bounds__(kBlock) k_estep_small(EArgs a) {
         auto loadpack = [&](int c) -> uint4 {
             return *reinterpret_cast<const uint4 *>(symw + (long long)c * U * kChunk);
         };
+        // Emission-table element of this lane for packed entry k.  With LDS tables the packs hold the
+        // byte offset of the symbol's row (o * GP * 8, precomputed on the host), else the symbol.
+        const char *tabj = reinterpret_cast<const char *>(Btab + j);
+        auto brow = [&](const uint4 &p, int k) -> const double * {
+            if constexpr (LDSTAB) return reinterpret_cast<const double *>(tabj + sym_of(p, k));
+            else return reinterpret_cast<const double *>(tabj) + (size_t)sym_of(p, k) * GP;
+        };
+        // One forward step: (A^T z_{t-1})_j * bs, bs = b_j(o_t) [* 2^-s_t].  Used verbatim by the
+        // forward sweep and by the backward recompute, so both produce bit-identical z_t.
+        auto step = [&](double zp, double bs) -> double {
+            if constexpr (LR) {
+                const double prev = dpp<0x111>(zp);  // row_shr:1 -> z_{t-1}(j-1); a_in = 0 for j = 0
+                return fma(a_in * bs, prev, (a_dg * bs) * zp);
+            } else {
+                double acc0 = 0.0, acc1 = 0.0;
+                sfor<0, N>([&](auto I) {
+                    const double zi = gbcast<G, I.value>(zp, lane);
+                    if constexpr ((I.value & 1) == 0) acc0 = fma(acol[I.value], zi, acc0);
+                    else acc1 = fma(acol[I.value], zi, acc1);
+                });
+                return (acc0 + acc1) * bs;
+            }
+        };
+        // Biased exponent field of the group's largest entry (entries are >= 0; 0 for an all-zero
+        // group).  Integer-only: bit-field extract + DPP max.
+        auto group_bexp = [&](double x) -> int {
+            return gmax_i32<G>((int)__builtin_amdgcn_ubfe((unsigned)__double2hiint(x), 20, 11));
+        };
 
-        // ---------------- forward: alpha_hat_t, e_t  (hmm_training.py:357-368) ----------------
-        double alpha = 0.0;
-        int E = 0;
-        uint4 pk = loadpack(0);
-        for (int c = 0; c < nch; ++c) {
-            const uint4 pkn = (c + 1 < nch) ? loadpack(c + 1) : pk;
+        // ---------------- forward sweep (hmm_training.py:357-368) ----------------
+        // Lagged mode: only steps t = 0 mod kScale rescale; s_t = M_{t-kScale}, the group exponent
+        // measured right after step t-kScale, so C_t = log2|alpha_{t-kScale}| and the stored z stay
+        // within a few steps' growth of 1.
+        double z = 0.0;
+        int C = 0;
+        auto forward = [&](auto SAFE_, auto RAG_) -> bool {
+            constexpr bool SAFE = decltype(SAFE_)::value;
+            constexpr bool RAG = decltype(RAG_)::value;
+            z = 0.0;
+            C = 0;
+            int pend[kChunk / kScale] = {};  // lagged: exponents to apply at the coming scale steps
+            int minM = 4096, maxM = 0;       // extreme group exponents seen (fallback trigger)
+            uint4 p0 = loadpack(0);
+            uint4 p1 = nch > 1 ? loadpack(1) : p0;
+            double bv[kChunk];
 #pragma unroll
-            for (int s = 0; s < kChunk; ++s) {
-                const int t = c * kChunk + s;
-                const int o = sym_of(pk, s);
-                const double b = Btab[o * G + j];
-                double x;
-                if (t == 0) {
-                    x = pij * b;                                            // :360
-                } else if constexpr (LR) {
-                    double prev = dpp<0x111>(alpha);                        // row_shr:1 -> alpha(j-1)
-                    prev = (j == 0) ? 0.0 : prev;
-                    x = fma(a_in, prev, a_dg * alpha) * b;                 // :141-156
-                } else {
-                    double acc0 = 0.0, acc1 = 0.0;
-                    sfor<0, N>([&](auto I) {
-                        const double ai = gbcast<G, I.value>(alpha, lane);
-                        if constexpr ((I.value & 1) == 0) acc0 = fma(acol[I.value], ai, acc0);
-                        else acc1 = fma(acol[I.value], ai, acc1);
-                    });
-                    x = (acc0 + acc1) * b;
-                }
-                const double sum = gsum<G>(x);
-                const int e = __builtin_amdgcn_frexp_exp(sum);  // 0 for sum == 0
-                x = pow2_scale(x, e);
-                if (t < T) {
-                    alpha = x;
-                    E += e;
-                    if constexpr (!FWD_ONLY) {
-                        aw[(long long)t * kWave] = x;
-                        if (j == 0) ew[(long long)t * U] = e;
-                    }
-                }
-            }
-            pk = pkn;
-        }
-        // log P(O|lambda) = log(sum_j alpha_hat_{T-1}(j)) + ln2 * sum_t e_t   (:375-377)
-        const double phat = gsum<G>(alpha);
-        const bool alive = (T > 0) && (phat > 0.0);
-        if (T > 0 && j == 0 && seq >= 0)
-            a.logp[seq] = alive ? (log(phat) + (double)E * 0.69314718055994530942) : -INFINITY;
-
-        if constexpr (!FWD_ONLY) {
-            // ---------------- backward sweep fused with gamma / xi / M-step numerators ----------
-            double beta = 1.0 / phat;  // beta_hat_{T-1} = 1/phat folds the 1/P of :392,:407
-            const int tl = T > 0 ? T - 1 : 0;
-            const int olast = symw[(long long)(tl / kChunk) * U * kChunk + (tl % kChunk)];
-            {
-                const double g = alpha * beta;  // gamma_{T-1}
-                if (alive) {
-                    gall = g;
-                    if (T == 1) pin = g;
-                    if (jv) {
-                        if constexpr (LDSTAB) atomicAdd(&sBn[olast * G + j], g);
-                        else unsafeAtomicAdd(&a.stats[a.off_bnum + (long long)olast * N + j], g);
-                    }
-                }
-            }
-            double ca[kChunk], na[kChunk];
-            int ce[kChunk], ne[kChunk];
-            const int clast = (Tw >= 2) ? (Tw - 2) / kChunk : -1;
-            if (clast >= 0) {
+            for (int k = 0; k < kChunk; ++k) bv[k] = *brow(p0, k);
+            auto chunk = [&](int c, auto MASK_) {
+                constexpr bool MASK = decltype(MASK_)::value;
+                const int Tend = RAG ? T : Tw;
+                int sp[kChunk];
 #pragma unroll
-                for (int s = 0; s < kChunk; ++s) {
-                    const long long t = (long long)clast * kChunk + s;
-                    ca[s] = aw[t * kWave];
-                    ce[s] = ew[(t + 1) * U];
-                }
-            }
-            uint4 pkhi = (clast + 1 < nch) ? loadpack(clast + 1) : pk;
-            for (int c = clast; c >= 0; --c) {
-                const uint4 pkc = loadpack(c);
-                const int cn = c > 0 ? c - 1 : 0;  // prefetch the next (lower) chunk
-#pragma unroll
-                for (int s = 0; s < kChunk; ++s) {
-                    const long long t = (long long)cn * kChunk + s;
-                    na[s] = aw[t * kWave];
-                    ne[s] = ew[(t + 1) * U];
-                }
-#pragma unroll
-                for (int s = kChunk - 1; s >= 0; --s) {
-                    const int t = c * kChunk + s;
-                    const int o1 = (s == kChunk - 1) ? sym_of(pkhi, 0) : sym_of(pkc, s + 1);
-                    const int o0 = sym_of(pkc, s);
-                    const double at = ca[s];
-                    const double b1 = Btab[o1 * G + j];
-                    const double v = pow2_scale(b1 * beta, ce[s]);  // b_j(o_{t+1}) beta_{t+1}(j) / c_{t+1}
-                    const bool act = alive && (t <= T - 2);
-                    double bn;
-                    if constexpr (LR) {
-                        double vup = dpp<0x101>(v);  // row_shl:1 -> v(j+1)
-                        vup = (j + 1 < N) ? vup : 0.0;
-                        bn = fma(a_up, vup, a_dg * v);       // :182-197
-                        if (act) {
-                            S[0] = fma(at, v, S[0]);         // xi_t(j,j)   / a_jj
-                            S[1] = fma(at, vup, S[1]);       // xi_t(j,j+1) / a_j,j+1
+                for (int k = 0; k < kChunk; ++k) {
+                    const int t = c * kChunk + k;
+                    double zn;
+                    int st = 0;
+                    if constexpr (SAFE) {
+                        const double x = (t == 0) ? pij * bv[k] : step(z, bv[k]);
+                        const int M = group_bexp(x);
+                        st = M == 0 ? 0 : M - 1023;
+                        zn = pow2_scale(x, st);
+                    } else if (k % kScale == 0) {
+                        st = pend[k / kScale];
+                        const double bs = pow2_scale(bv[k], st);
+                        zn = (t == 0) ? pij * bs : step(z, bs);
+                        const int M = group_bexp(zn);
+                        // applied kScale steps later; clamped so an all-zero (dead) group can never
+                        // scale itself to inf (the fallback below catches it)
+                        pend[k / kScale] = min(max(M - 1023, -600), 600);
+                        if (!RAG || t < T) {
+                            minM = min(minM, M);
+                            maxM = max(maxM, M);
                         }
                     } else {
-                        double b0 = 0.0, bb = 0.0;
-                        sfor<0, N>([&](auto I) {
-                            const double vk = gbcast<G, I.value>(v, lane);
-                            if constexpr ((I.value & 1) == 0) b0 = fma(arow[I.value], vk, b0);
-                            else bb = fma(arow[I.value], vk, bb);
-                            if (act) S[I.value] = fma(at, vk, S[I.value]);   // :402-408
-                        });
-                        bn = b0 + bb;
+                        zn = step(z, bv[k]);
                     }
-                    if (act) {
-                        const double g = at * bn;  // gamma_t(j)  (:392)
-                        beta = bn;
-                        gex += g;
-                        if (t == 0) pin = g;
-                        if (jv) {
-                            if constexpr (LDSTAB) atomicAdd(&sBn[o0 * G + j], g);   // :474-485
-                            else unsafeAtomicAdd(&a.stats[a.off_bnum + (long long)o0 * N + j], g);
+                    if constexpr (MASK) {
+                        const bool act = t < Tend;
+                        z = act ? zn : z;
+                        C += act ? st : 0;
+                    } else {
+                        z = zn;
+                        C += st;
+                    }
+                    sp[k] = st;
+                    if constexpr (!FWD_ONLY)
+                        if (k == 0) ckw[(long long)c * kWave] = z;  // checkpoint z_{8c}
+                }
+                if constexpr (!FWD_ONLY) spw[(long long)c * U] = pack_exps(sp);
+            };
+            for (int c = 0; c < nch; ++c) {
+                const uint4 p2 = (c + 2 < nch) ? loadpack(c + 2) : p1;
+                double bvn[kChunk];  // next chunk's emissions, in flight during this chunk
+#pragma unroll
+                for (int k = 0; k < kChunk; ++k) bvn[k] = *brow(p1, k);
+                if (RAG || (c == nch - 1 && (Tw % kChunk) != 0)) chunk(c, std::true_type{});
+                else chunk(c, std::false_type{});
+#pragma unroll
+                for (int k = 0; k < kChunk; ++k) bv[k] = bvn[k];
+                p0 = p1;
+                p1 = p2;
+            }
+            return (!SAFE) && (minM < 1023 - 900 || maxM > 1023 + 900);
+        };
+        bool safe = a.force_safe != 0;
+        if (!safe) {
+            const bool bad = full ? forward(std::false_type{}, std::false_type{})
+                                  : forward(std::false_type{}, std::true_type{});
+            safe = __any(bad && T > 0) != 0;  // wave-uniform: redo the wave with per-step normalisation
+        }
+        if (safe) {
+            if (full) forward(std::true_type{}, std::false_type{});
+            else forward(std::true_type{}, std::true_type{});
+        }
+
+        // log P(O|lambda) = log(sum_j z_{T-1}(j)) + ln2 * C   (:375-377)
+        const double phat = gsum<G>(z);
+        const bool alive = (T > 0) && (phat > 0.0);
+        const double lp = alive ? (log(phat) + (double)C * 0.69314718055994530942) : -INFINITY;
+        if (T > 0 && j == 0 && seq >= 0) a.logp[seq] = lp;
+        logp_lane = lp;
+        ll_valid = (T > 0) && (j == 0);
+
+        if constexpr (!FWD_ONLY) if (!(a.ablate & 2)) {
+            // ------------- backward sweep fused with gamma / xi / M-step numerators -------------
+            const double inv_p = alive ? 1.0 / phat : 0.0;  // beta_hat_{T-1}: folds 1/P (:392,:407)
+            auto backward = [&](auto SAFE_, auto RAG_) {
+                constexpr bool SAFE = decltype(SAFE_)::value;
+                constexpr bool RAG = decltype(RAG_)::value;
+                double beta = inv_p;
+                const int cl = (Tw - 1) / kChunk;
+                auto ldck = [&](int c) { return ckw[(long long)c * kWave]; };
+                auto ldsp = [&](int c) { return spw[(long long)c * U]; };
+                double ckA = ldck(cl), ckB = ldck(cl >= 1 ? cl - 1 : 0);
+                uint4 spA = ldsp(cl), spB = ldsp(cl >= 1 ? cl - 1 : 0);
+                uint4 pkA = loadpack(cl), pkB = loadpack(cl >= 1 ? cl - 1 : 0);
+                double bv[kChunk], bu[kChunk];
+                auto ldrows = [&](const uint4 &p) {
+#pragma unroll
+                    for (int k = 0; k < kChunk; ++k) {
+                        const double *r = brow(p, k);
+                        bv[k] = r[0];
+                        if constexpr (LR) bu[k] = r[1];  // b_{j+1}(o): the neighbour's emission
+                    }
+                };
+                ldrows(pkA);
+                double f_hi = 0.0, fu_hi = 0.0;  // scaled emissions at o_{8c+8} (from chunk c+1)
+                auto chunk = [&](int c, auto MASK_) {
+                    constexpr bool MASK = decltype(MASK_)::value;
+                    int sk[kChunk];
+                    double fs[kChunk], fus[kChunk];  // b(o_t) / c_t for t = 8c .. 8c+7
+#pragma unroll
+                    for (int k = 0; k < kChunk; ++k) {
+                        const bool scaled = SAFE || (k % kScale == 0);
+                        sk[k] = scaled ? exp_of(spA, k) : 0;
+                        fs[k] = scaled ? pow2_scale(bv[k], sk[k]) : bv[k];
+                        if constexpr (LR) fus[k] = scaled ? pow2_scale(bu[k], sk[k]) : bu[k];
+                    }
+                    // recompute z_{8c .. 8c+7} from the checkpoint (identical ops to the forward)
+                    double zr[kChunk];
+                    zr[0] = ckA;
+#pragma unroll
+                    for (int k = 1; k < kChunk; ++k) {
+                        if constexpr (SAFE) zr[k] = pow2_scale(step(zr[k - 1], bv[k]), sk[k]);
+                        else zr[k] = step(zr[k - 1], fs[k]);
+                    }
+                    double gk[kChunk];
+#pragma unroll
+                    for (int k = kChunk - 1; k >= 0; --k) {
+                        const int t = c * kChunk + k;
+                        const double f = (k == kChunk - 1) ? f_hi : fs[k + 1];  // b(o_{t+1}) / c_{t+1}
+                        const double zt = zr[k];
+                        // regular step (t <= T-2) / gamma_{T-1} (t == T-1) / past the end; per lane in
+                        // ragged waves, wave-uniform otherwise; only boundary chunks are masked.
+                        // zs = 0 leaves S and gex unchanged.
+                        const bool reg = !MASK || (RAG ? (t <= T - 2) : (t <= Tw - 2));
+                        const bool ini = MASK && (RAG ? (t == T - 1) : (t == Tw - 1));
+                        const double zs = reg ? zt : 0.0;
+                        double bn;
+                        if constexpr (LR) {
+                            const double fu = (k == kChunk - 1) ? fu_hi : fus[k + 1];
+                            const double bup = dpp<0x101>(beta);  // row_shl:1 -> beta(j+1)
+                            const double vd = f * beta, vu = fu * bup;
+                            bn = fma(a_up, vu, a_dg * vd);       // :182-197
+                            S[0] = fma(zs, vd, S[0]);             // xi_t(j,j)   / a_jj
+                            S[1] = fma(zs, vu, S[1]);             // xi_t(j,j+1) / a_j,j+1
+                        } else {
+                            const double vd = f * beta;
+                            double b0 = 0.0, b1 = 0.0;
+                            sfor<0, N>([&](auto I) {
+                                const double vk = gbcast<G, I.value>(vd, lane);
+                                if constexpr ((I.value & 1) == 0) b0 = fma(arow[I.value], vk, b0);
+                                else b1 = fma(arow[I.value], vk, b1);
+                                S[I.value] = fma(zs, vk, S[I.value]);   // :402-408
+                            });
+                            bn = b0 + b1;
+                        }
+                        double g;  // gamma_t(j) (:392)
+                        if constexpr (MASK) {
+                            g = reg ? zt * bn : (ini ? zt * inv_p : 0.0);
+                            beta = reg ? bn : beta;
+                            gex = fma(zs, bn, gex);
+                            gall += ini ? g : 0.0;
+                        } else {
+                            g = zt * bn;
+                            beta = bn;
+                            gex += g;
+                        }
+                        if (t == 0) pin = g;  // :420
+                        gk[k] = g;
+                    }
+                    // next chunk's emission rows go to LDS before this chunk's histogram atomics, so
+                    // they are not queued behind them
+                    ldrows(pkB);
+                    if ((N == G || jv) && !(a.ablate & 4)) {
+#pragma unroll
+                        for (int k = 0; k < kChunk; ++k) {  // :474-485
+                            if constexpr (LDSTAB) {
+                                atomicAdd(reinterpret_cast<double *>(reinterpret_cast<char *>(sBn + j) + sym_of(pkA, k)), gk[k]);
+                            } else if (gk[k] != 0.0) {
+                                unsafeAtomicAdd(&accb[a.off_bnum + (long long)sym_of(pkA, k) * N + j], gk[k]);
+                            }
                         }
                     }
+                    f_hi = fs[0];
+                    if constexpr (LR) fu_hi = fus[0];
+                };
+                for (int c = cl; c >= 0; --c) {
+                    const int cn = c >= 2 ? c - 2 : 0;  // global prefetch two chunks ahead
+                    const double ckC = ldck(cn);
+                    const uint4 spC = ldsp(cn), pkC = loadpack(cn);
+                    if (RAG || c == cl) chunk(c, std::true_type{});
+                    else chunk(c, std::false_type{});
+                    ckA = ckB; spA = spB; pkA = pkB;
+                    ckB = ckC; spB = spC; pkB = pkC;
                 }
-                pkhi = pkc;
-#pragma unroll
-                for (int s = 0; s < kChunk; ++s) { ca[s] = na[s]; ce[s] = ne[s]; }
+            };
+            if (safe) {
+                if (full) backward(std::true_type{}, std::false_type{});
+                else backward(std::true_type{}, std::true_type{});
+            } else {
+                if (full) backward(std::false_type{}, std::false_type{});
+                else backward(std::false_type{}, std::true_type{});
             }
             gall += gex;
         }
     }
 
-    if constexpr (!FWD_ONLY) {
+    // per-block (max, sum exp) of log P for the convergence scalar
+    __syncthreads();
+    block_ll_partial(logp_lane, ll_valid, sRed, a.llpart + 2 * (long long)blockIdx.x);
+
+    if constexpr (!FWD_ONLY) if (!(a.ablate & 1)) {
         // ---- reduce per-lane accumulators over the U sequences of the wave, then the block ----
         double vals[NV];
 #pragma unroll
@@ -351,6 +563,7 @@ __global__ void __launch_bounds__(kBlock) k_estep_small(EArgs a) {
             for (int m = G; m < kWave; m <<= 1) x += __shfl_xor(x, m);
             vals[k] = x;
         }
+        __syncthreads();
         if (u == 0) {
 #pragma unroll
             for (int k = 0; k < NV; ++k) sRed[(wv * G + j) * NV + k] = vals[k];
@@ -375,14 +588,14 @@ __global__ void __launch_bounds__(kBlock) k_estep_small(EArgs a) {
             } else {
                 dst = jj;  // pi_num at offset 0
             }
-            unsafeAtomicAdd(&a.stats[dst], x);
+            unsafeAtomicAdd(&accb[dst], x);
         }
         if constexpr (LDSTAB) {
             for (int idx = tid; idx < K * G; idx += blockDim.x) {
-                const int jj = idx & (G - 1);
+                const int k = idx / G, jj = idx - k * G;
                 if (jj >= N) continue;
-                const double x = sBn[idx];
-                if (x != 0.0) unsafeAtomicAdd(&a.stats[a.off_bnum + (long long)(idx / G) * N + jj], x);
+                const double x = sBn[k * GP + jj];
+                if (x != 0.0) unsafeAtomicAdd(&accb[a.off_bnum + (long long)k * N + jj], x);
             }
         }
     }
@@ -408,14 +621,18 @@ __global__ void __launch_bounds__(kBlock) k_estep_wide(EArgs a) {
     }
     __syncthreads();
     const long long wave = (long long)blockIdx.x * (blockDim.x >> 6) + wv;
+    double *accb = a.copies + (long long)(blockIdx.x % a.ncopies) * a.copy_len;
+    double logp_lane = -INFINITY;
+    bool ll_valid = false;
+    [&]() {
     if (wave >= a.L.nwaves) return;
     const int T = a.L.slot_len[wave];
     const int seq = a.L.slot_seq[wave];
     if (T <= 0) return;
     const int nch = (T + kChunk - 1) / kChunk;
     const uint16_t *symw = a.L.sym + a.L.wave_symoff[wave];
-    double *aw = a.alpha + (FWD_ONLY ? 0 : a.L.wave_aoff[wave]) + lane;
-    int *ew = a.ebuf + (FWD_ONLY ? 0 : a.L.wave_eoff[wave]);
+    double *aw = a.ckpt + (FWD_ONLY ? 0 : a.L.wave_ckoff[wave]) + lane;
+    int *ew = a.ebuf + (FWD_ONLY ? 0 : a.L.wave_spoff[wave]);
     const bool jv = j < N;
     const double pij = jv ? a.pi[j] : 0.0;
     auto loadpack = [&](int c) -> uint4 { return *reinterpret_cast<const uint4 *>(symw + (long long)c * kChunk); };
@@ -464,7 +681,10 @@ __global__ void __launch_bounds__(kBlock) k_estep_wide(EArgs a) {
     }
     const double phat = gsum<64>(alpha);
     const bool alive = phat > 0.0;
-    if (j == 0 && seq >= 0) a.logp[seq] = alive ? (log(phat) + (double)E * 0.69314718055994530942) : -INFINITY;
+    const double lp = alive ? (log(phat) + (double)E * 0.69314718055994530942) : -INFINITY;
+    if (j == 0 && seq >= 0) a.logp[seq] = lp;
+    logp_lane = lp;
+    ll_valid = j == 0;
     if constexpr (!FWD_ONLY) {
         if (!alive) return;
         double S[NP];
@@ -476,7 +696,7 @@ __global__ void __launch_bounds__(kBlock) k_estep_wide(EArgs a) {
         const double glast = alpha * beta;
         double gall = glast;
         if (T == 1) pin = glast;
-        if (jv) unsafeAtomicAdd(&a.stats[a.off_bnum + (long long)symat(T - 1) * N + j], glast);
+        if (jv) unsafeAtomicAdd(&accb[a.off_bnum + (long long)symat(T - 1) * N + j], glast);
         int o1 = symat(T - 1);
         for (int t = T - 2; t >= 0; --t) {
             const int o0 = symat(t);
@@ -499,19 +719,22 @@ __global__ void __launch_bounds__(kBlock) k_estep_wide(EArgs a) {
             beta = bn;
             gex += g;
             if (t == 0) pin = g;
-            if (jv) unsafeAtomicAdd(&a.stats[a.off_bnum + (long long)o0 * N + j], g);
+            if (jv) unsafeAtomicAdd(&accb[a.off_bnum + (long long)o0 * N + j], g);
             o1 = o0;
         }
         gall += gex;
         if (jv) {
 #pragma unroll
             for (int k = 0; k < NP; ++k)
-                if (k < N && S[k] != 0.0) unsafeAtomicAdd(&a.stats[a.off_S + (long long)j * N + k], S[k]);
-            if (gex != 0.0) unsafeAtomicAdd(&a.stats[a.off_gex + j], gex);
-            if (gall != 0.0) unsafeAtomicAdd(&a.stats[a.off_gall + j], gall);
-            if (pin != 0.0) unsafeAtomicAdd(&a.stats[j], pin);
+                if (k < N && S[k] != 0.0) unsafeAtomicAdd(&accb[a.off_S + (long long)j * N + k], S[k]);
+            if (gex != 0.0) unsafeAtomicAdd(&accb[a.off_gex + j], gex);
+            if (gall != 0.0) unsafeAtomicAdd(&accb[a.off_gall + j], gall);
+            if (pin != 0.0) unsafeAtomicAdd(&accb[j], pin);
         }
     }
+    }();
+    __syncthreads();
+    block_ll_partial(logp_lane, ll_valid, smem + 2 * NP * 64 + 4 * 64, a.llpart + 2 * (long long)blockIdx.x);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -541,40 +764,60 @@ __device__ double block_reduce(double x, double *sh, bool is_max) {
     return r;
 }
 
-// (max, sum exp(x - max)) over the finite log P_r of this rank  (log_sum_exp :66-79 over :503)
-__device__ void seq_lse_pair(const double *logp, long long R, double *sh, double *m_out, double *s_out) {
+// Combine per-block (max, sum exp) pairs into this rank's pair (log_sum_exp :66-79 over :503).
+__device__ void combine_ll_pairs(const double *pairs, long long n, double *sh, double *m_out, double *s_out) {
     double mx = -INFINITY;
-    for (long long r = threadIdx.x; r < R; r += blockDim.x) mx = fmax(mx, logp[r]);
+    for (long long r = threadIdx.x; r < n; r += blockDim.x)
+        if (pairs[2 * r + 1] > 0.0) mx = fmax(mx, pairs[2 * r]);
     mx = block_reduce(mx, sh, true);
     double s = 0.0;
     if (mx != -INFINITY)
-        for (long long r = threadIdx.x; r < R; r += blockDim.x) {
-            const double x = logp[r];
-            if (x != -INFINITY) s += exp(x - mx);
+        for (long long r = threadIdx.x; r < n; r += blockDim.x) {
+            const double sr = pairs[2 * r + 1];
+            if (sr > 0.0) s += sr * exp(pairs[2 * r] - mx);
         }
     s = block_reduce(s, sh, false);
     *m_out = mx;
     *s_out = s;
 }
 
-__global__ void __launch_bounds__(1024) k_seq_lse(const double *logp, long long R, double *stats, long long off_ll,
-                                                  int rank, const IterState *state) {
+// Multi-rank: sum this rank's statistics copies into the caller's buffer (for the all-reduce),
+// zero the copies, and write the rank's (max, sum exp) pair of log P into its slot.
+__global__ void __launch_bounds__(256) k_reduce_local(double *copies, int ncopies, long long copy_len,
+                                                      const double *llpart, long long nblocks, double *stats,
+                                                      long long off_ll, int world, int rank,
+                                                      const IterState *state) {
     __shared__ double sh[16];
     if (state->done) return;
-    double m, s;
-    seq_lse_pair(logp, R, sh, &m, &s);
-    if (threadIdx.x == 0) {
-        stats[off_ll + 2 * rank] = (s > 0.0) ? m : 0.0;
-        stats[off_ll + 2 * rank + 1] = s;
+    for (long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x; idx < copy_len;
+         idx += (long long)gridDim.x * blockDim.x) {
+        double v = 0.0;
+        for (int c = 0; c < ncopies; ++c) {
+            v += copies[c * copy_len + idx];
+            copies[c * copy_len + idx] = 0.0;
+        }
+        stats[idx] = v;
+    }
+    if (blockIdx.x == 0) {
+        double m, s;
+        combine_ll_pairs(llpart, nblocks, sh, &m, &s);
+        if (threadIdx.x < 2 * world) stats[off_ll + threadIdx.x] = 0.0;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            stats[off_ll + 2 * rank] = (s > 0.0) ? m : 0.0;
+            stats[off_ll + 2 * rank + 1] = s;
+        }
     }
 }
 
 struct MArgs {
-    double *stats;
-    long long stats_len;
+    const double *src;     // statistics: the copies (single rank) or the all-reduced buffer
+    double *zero_ll;       // LL slots to clear (multi-rank) or nullptr
+    int nsrc;
+    long long copy_len;
     double *pi, *A, *B, *Bt;
-    const double *logp;
-    long long R_local;
+    const double *llpart;
+    long long nblocks;
     long long R_global;
     IterState *state;
     double *hist;
@@ -583,50 +826,63 @@ struct MArgs {
     long long off_S, off_gex, off_gall, off_bnum, off_ll;
 };
 
-__global__ void __launch_bounds__(1024) k_mstep(MArgs m) {
+// sum of one statistic over the copies, clearing them for the next iteration
+__device__ __forceinline__ double take(const MArgs &m, long long idx) {
+    double v = 0.0;
+    double *p = const_cast<double *>(m.src) + idx;
+    for (int c = 0; c < m.nsrc; ++c) {
+        v += p[c * m.copy_len];
+        p[c * m.copy_len] = 0.0;
+    }
+    return v;
+}
+
+__global__ void __launch_bounds__(256) k_mstep(MArgs m) {
     __shared__ double sh[16];
     __shared__ double sL;
+    __shared__ double sPi[64], sGex[64], sGall[64];
     IterState *st = m.state;
     if (st->done) return;
     const int tid = threadIdx.x;
     // L = LSE_r log P_r over all ranks (:503)
     if (m.local_lse) {
         double mx, s;
-        seq_lse_pair(m.logp, m.R_local, sh, &mx, &s);
+        combine_ll_pairs(m.llpart, m.nblocks, sh, &mx, &s);
         if (tid == 0) sL = (s > 0.0) ? mx + log(s) : -INFINITY;
     } else if (tid == 0) {
+        const double *ll = m.src + m.off_ll;
         double mx = -INFINITY;
         for (int r = 0; r < m.world; ++r)
-            if (m.stats[m.off_ll + 2 * r + 1] > 0.0) mx = fmax(mx, m.stats[m.off_ll + 2 * r]);
+            if (ll[2 * r + 1] > 0.0) mx = fmax(mx, ll[2 * r]);
         double s = 0.0;
         if (mx != -INFINITY)
-            for (int r = 0; r < m.world; ++r) {
-                const double sr = m.stats[m.off_ll + 2 * r + 1];
-                if (sr > 0.0) s += sr * exp(m.stats[m.off_ll + 2 * r] - mx);
-            }
+            for (int r = 0; r < m.world; ++r)
+                if (ll[2 * r + 1] > 0.0) s += ll[2 * r + 1] * exp(ll[2 * r] - mx);
         sL = (s > 0.0) ? mx + log(s) : -INFINITY;
+        for (int r = 0; r < 2 * m.world; ++r) m.zero_ll[r] = 0.0;
     }
     const int N = m.N, K = m.K;
-    const double *st_ = m.stats;
-    // pi (:415-424): LSE_r gamma_0 - log R ; no term -> -inf
     for (int i = tid; i < N; i += blockDim.x) {
-        const double num = st_[i];
-        m.pi[i] = num > 0.0 ? num / (double)m.R_global : 0.0;
+        sPi[i] = take(m, i);
+        sGex[i] = take(m, m.off_gex + i);
+        sGall[i] = take(m, m.off_gall + i);
     }
+    __syncthreads();
+    // pi (:415-424): LSE_r gamma_0 - log R ; no term -> -inf
+    for (int i = tid; i < N; i += blockDim.x) m.pi[i] = sPi[i] > 0.0 ? sPi[i] / (double)m.R_global : 0.0;
     // A (:429-455): xi numerator = a_ij * S_ij ; denominator excludes the last frame
     for (int idx = tid; idx < N * N; idx += blockDim.x) {
-        const int i = idx / N;
-        const double den = st_[m.off_gex + i];
-        const double num = m.A[idx] * st_[m.off_S + idx];
+        const double den = sGex[idx / N];
+        const double num = m.A[idx] * take(m, m.off_S + idx);
         m.A[idx] = (den > 0.0 && num > 0.0) ? num / den : 0.0;
     }
     // B (:460-497): floor 1e-20 when no gamma term carries the symbol; empty denominator -> row 0
     for (long long idx = tid; idx < (long long)N * K; idx += blockDim.x) {
-        const int jj = (int)(idx / K), k = (int)(idx % K);
-        const double den = st_[m.off_gall + jj];
-        const double num = st_[m.off_bnum + (long long)k * N + jj];
+        const int jj = (int)(idx % N), k = (int)(idx / N);  // symbol-major: coalesced over the copies
+        const double den = sGall[jj];
+        const double num = take(m, m.off_bnum + idx);
         const double v = den > 0.0 ? (num > 0.0 ? num / den : 1e-20) : 0.0;
-        m.B[idx] = v;
+        m.B[(long long)jj * K + k] = v;
         m.Bt[(long long)k * m.G + jj] = v;
     }
     __syncthreads();
@@ -647,8 +903,6 @@ __global__ void __launch_bounds__(1024) k_mstep(MArgs m) {
             st->converged = (it + 1 < st->max_iterations) ? 1 : 0;
         }
     }
-    // zero the statistics for the next iteration
-    for (long long idx = tid; idx < m.stats_len; idx += blockDim.x) m.stats[idx] = 0.0;
 }
 
 // safe_exp + normalisation of the returned parameters (:524-541)
@@ -759,16 +1013,21 @@ struct hmmbw_ctx {
     // training state
     IterState *d_state = nullptr;
     double *d_hist = nullptr;
-    double *d_stats = nullptr;
+    double *d_copies = nullptr;   // [ncopies][copy_len] E-step accumulators
+    int ncopies = 1;
     bool armed = false;
     // observations
     long long R = 0, nwaves = 0;
+    long long nblocks = 0;
     uint16_t *d_sym = nullptr;
-    long long *d_wsym = nullptr, *d_waoff = nullptr, *d_weoff = nullptr;
-    int *d_wT = nullptr, *d_slen = nullptr, *d_sseq = nullptr;
-    double *d_alpha = nullptr, *d_logp = nullptr;
+    long long *d_wsym = nullptr, *d_wckoff = nullptr, *d_wspoff = nullptr;
+    int *d_wT = nullptr, *d_wfull = nullptr, *d_slen = nullptr, *d_sseq = nullptr;
+    double *d_ck = nullptr, *d_logp = nullptr, *d_llpart = nullptr;
+    uint4 *d_sp = nullptr;
     int *d_ebuf = nullptr;
     bool has_obs = false;
+    int force_safe = 0;
+    int ablate = 0;
     // timing
     bool timing = false;
     std::vector<hipEvent_t> ev_free, ev_pending;  // pairs (start, stop)
@@ -781,7 +1040,9 @@ struct hmmbw_ctx {
     long long off_bnum() const { return off_gall() + N; }
     long long off_ll() const { return off_bnum() + (long long)K * N; }
     long long stats_len() const { return off_ll() + 2LL * world; }
-    bool lds_tables() const { return !wide && (size_t)2 * K * G * sizeof(double) <= 48 * 1024; }
+    long long copy_len() const { return off_ll(); }
+    // emission table + B-numerator histogram in LDS ([K][G+1] fp64 each) when they fit 48 KiB
+    bool lds_tables() const { return !wide && (size_t)(2 * K + 1) * (G + 1) * sizeof(double) <= 48 * 1024; }
 };
 
 namespace {
@@ -791,23 +1052,38 @@ int set_device(hmmbw_ctx *c) {
     return HMMBW_OK;
 }
 
+void free_obs(hmmbw_ctx *c) {
+    dfree(c->d_sym); dfree(c->d_wsym); dfree(c->d_wckoff); dfree(c->d_wspoff);
+    dfree(c->d_wT); dfree(c->d_wfull); dfree(c->d_slen); dfree(c->d_sseq);
+    dfree(c->d_ck); dfree(c->d_sp); dfree(c->d_ebuf); dfree(c->d_logp); dfree(c->d_llpart);
+    c->has_obs = false;
+}
+
 int realloc_stats(hmmbw_ctx *c) {
-    dfree(c->d_stats);
-    if (int rc = dalloc(&c->d_stats, (size_t)c->stats_len())) return rc;
-    HIP_TRY(hipMemsetAsync(c->d_stats, 0, sizeof(double) * c->stats_len(), c->stream));
+    dfree(c->d_copies);
+    const size_t n = (size_t)c->ncopies * c->copy_len();
+    if (int rc = dalloc(&c->d_copies, n)) return rc;
+    HIP_TRY(hipMemsetAsync(c->d_copies, 0, sizeof(double) * n, c->stream));
     return HMMBW_OK;
 }
 
-EArgs make_eargs(hmmbw_ctx *c, double *stats) {
+EArgs make_eargs(hmmbw_ctx *c) {
     EArgs a{};
-    a.L = Layout{c->d_sym, c->d_wsym, c->d_waoff, c->d_weoff, c->d_wT, c->d_slen, c->d_sseq, c->nwaves};
+    a.L = Layout{c->d_sym, c->d_wsym, c->d_wckoff, c->d_wspoff, c->d_wT, c->d_wfull, c->d_slen, c->d_sseq,
+                 c->nwaves};
     a.pi = c->d_pi;
     a.A = c->d_A;
     a.Bt = c->d_Bt;
-    a.alpha = c->d_alpha;
+    a.ckpt = c->d_ck;
+    a.spack = c->d_sp;
     a.ebuf = c->d_ebuf;
-    a.stats = stats;
+    a.copies = c->d_copies;
+    a.copy_len = c->copy_len();
+    a.ncopies = c->ncopies;
     a.logp = c->d_logp;
+    a.llpart = c->d_llpart;
+    a.force_safe = c->force_safe;
+    a.ablate = c->ablate;
     a.state = c->d_state;
     a.K = c->K;
     a.N = c->N;
@@ -828,8 +1104,8 @@ int launch_lds(F f, unsigned grid, size_t lds, hipStream_t stream, const EArgs &
     return HMMBW_OK;
 }
 
-int launch_estep(hmmbw_ctx *c, double *stats, bool fwd_only, const IterState *state) {
-    EArgs a = make_eargs(c, stats);
+int launch_estep(hmmbw_ctx *c, bool fwd_only, const IterState *state) {
+    EArgs a = make_eargs(c);
     a.state = state;
     const int wpb = kBlock / kWave;
     const unsigned grid = (unsigned)((c->nwaves + wpb - 1) / wpb);
@@ -848,7 +1124,7 @@ int launch_estep(hmmbw_ctx *c, double *stats, bool fwd_only, const IterState *st
         HIP_TRY(hipEventRecord(e0, c->stream));
     }
     if (c->wide) {
-        const size_t lds = sizeof(double) * (2 * (size_t)c->NP * 64 + (size_t)wpb * 64);
+        const size_t lds = sizeof(double) * (2 * (size_t)c->NP * 64 + (size_t)wpb * 64 + 8);
         KernelFn f = c->NP == 32 ? (fwd_only ? k_estep_wide<32, true> : k_estep_wide<32, false>)
                                  : (fwd_only ? k_estep_wide<64, true> : k_estep_wide<64, false>);
         if (int rc = launch_lds(f, grid, lds, c->stream, a)) return rc;
@@ -860,7 +1136,9 @@ int launch_estep(hmmbw_ctx *c, double *stats, bool fwd_only, const IterState *st
         KernelFn f = fwd_only ? ks.score : ks.estep;
         if (!f) return fail(HMMBW_E_UNSUPPORTED, "no kernel for N");
         const int NV = (lr ? 2 : c->N) + 3;
-        const size_t lds = sizeof(double) * ((lds_tab ? 2 * (size_t)c->K * c->G : 0) + (size_t)wpb * c->G * NV);
+        const size_t GP = (size_t)c->G + 1;
+        const size_t tabs = lds_tab ? ((size_t)c->K + 1) * GP + (fwd_only ? 0 : (size_t)c->K * GP) : 0;
+        const size_t lds = sizeof(double) * (tabs + (size_t)wpb * c->G * NV + 8);
         if (int rc = launch_lds(f, grid, lds, c->stream, a)) return rc;
     }
     if (e1) {
@@ -885,16 +1163,19 @@ int drain_timing(hmmbw_ctx *c) {
     return HMMBW_OK;
 }
 
+// local: the statistics are this context's copies; otherwise the caller's all-reduced buffer
 int launch_mstep(hmmbw_ctx *c, double *stats, long long R_global, bool local) {
     MArgs m{};
-    m.stats = stats;
-    m.stats_len = c->stats_len();
+    m.src = local ? c->d_copies : stats;
+    m.zero_ll = local ? nullptr : stats + c->off_ll();
+    m.nsrc = local ? c->ncopies : 1;
+    m.copy_len = c->copy_len();
     m.pi = c->d_pi;
     m.A = c->d_A;
     m.B = c->d_B;
     m.Bt = c->d_Bt;
-    m.logp = c->d_logp;
-    m.R_local = c->R;
+    m.llpart = c->d_llpart;
+    m.nblocks = c->nblocks;
     m.R_global = R_global;
     m.state = c->d_state;
     m.hist = c->d_hist;
@@ -908,7 +1189,7 @@ int launch_mstep(hmmbw_ctx *c, double *stats, long long R_global, bool local) {
     m.off_gall = c->off_gall();
     m.off_bnum = c->off_bnum();
     m.off_ll = c->off_ll();
-    hipLaunchKernelGGL(k_mstep, dim3(1), dim3(1024), 0, c->stream, m);
+    hipLaunchKernelGGL(k_mstep, dim3(1), dim3(256), 0, c->stream, m);
     HIP_TRY(hipGetLastError());
     return HMMBW_OK;
 }
@@ -968,7 +1249,7 @@ int hmmbw_ctx_create(int device, int n_states, int n_symbols, hmmbw_ctx **out) {
     if (!rc) rc = dalloc(&c->d_pi, c->N);
     if (!rc) rc = dalloc(&c->d_A, (size_t)c->N * c->N);
     if (!rc) rc = dalloc(&c->d_B, (size_t)c->N * c->K);
-    if (!rc) rc = dalloc(&c->d_Bt, (size_t)c->K * c->G);
+    if (!rc) rc = dalloc(&c->d_Bt, (size_t)c->K * c->G + c->G);
     if (!rc) rc = dalloc(&c->d_out, (size_t)c->N + (size_t)c->N * c->N + (size_t)c->N * c->K);
     if (!rc) rc = dalloc(&c->d_state, 1);
     if (!rc) rc = dalloc(&c->d_hist, 2 * (size_t)kHist);
@@ -992,10 +1273,8 @@ int hmmbw_ctx_destroy(hmmbw_ctx *c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     else (void)hipDeviceSynchronize();
     dfree(c->d_pi); dfree(c->d_A); dfree(c->d_B); dfree(c->d_Bt); dfree(c->d_out);
-    dfree(c->d_state); dfree(c->d_hist); dfree(c->d_stats);
-    dfree(c->d_sym); dfree(c->d_wsym); dfree(c->d_waoff); dfree(c->d_weoff);
-    dfree(c->d_wT); dfree(c->d_slen); dfree(c->d_sseq);
-    dfree(c->d_alpha); dfree(c->d_logp); dfree(c->d_ebuf);
+    dfree(c->d_state); dfree(c->d_hist); dfree(c->d_copies);
+    free_obs(c);
     for (auto e : c->ev_free) (void)hipEventDestroy(e);
     for (auto e : c->ev_pending) (void)hipEventDestroy(e);
     delete c;
@@ -1045,7 +1324,7 @@ int hmmbw_set_observations(hmmbw_ctx *c, const int64_t *offsets, const int32_t *
         const int64_t T = offsets[r + 1] - offsets[r];
         if (T < 0) return fail(HMMBW_E_INVALID, "offsets must be non-decreasing");
         if (T == 0) return fail(HMMBW_E_EMPTY_SEQUENCE, "sequence " + std::to_string(r) + " is empty");
-        if (T > (1 << 30)) return fail(HMMBW_E_UNSUPPORTED, "sequence too long");
+        if (T > (1 << 28)) return fail(HMMBW_E_UNSUPPORTED, "sequence too long");
         len[(size_t)r] = (int)T;
     }
     const int64_t total = offsets[R];
@@ -1055,34 +1334,47 @@ int hmmbw_set_observations(hmmbw_ctx *c, const int64_t *offsets, const int32_t *
                                                   std::to_string(i) + " is outside [0, M)");
     if (int rc = set_device(c)) return rc;
     HIP_TRY(hipStreamSynchronize(c->stream));  // buffers may still be in use by enqueued work
-    // length-sorted (descending, stable) assignment of sequences to wave slots
+    // length-sorted (descending, stable) assignment of sequences to wave slots: the sequences that
+    // share a wave have near-equal lengths, so the lockstep time loop wastes little
     std::vector<int64_t> perm((size_t)R);
     std::iota(perm.begin(), perm.end(), 0);
     std::stable_sort(perm.begin(), perm.end(), [&](int64_t x, int64_t y) { return len[x] > len[y]; });
     const int U = c->U;
     const long long nwaves = (R + U - 1) / U;
-    std::vector<long long> wsym((size_t)nwaves), waoff((size_t)nwaves), weoff((size_t)nwaves);
-    std::vector<int> wT((size_t)nwaves), slen((size_t)(nwaves * U), 0), sseq((size_t)(nwaves * U), -1);
-    long long symtot = 0, atot = 0, etot = 0;
+    std::vector<long long> wsym((size_t)nwaves), wck((size_t)nwaves), wsp((size_t)nwaves);
+    std::vector<int> wT((size_t)nwaves), wfull((size_t)nwaves), slen((size_t)(nwaves * U), 0),
+        sseq((size_t)(nwaves * U), -1);
+    long long symtot = 0, cktot = 0, sptot = 0;
     for (long long w = 0; w < nwaves; ++w) {
-        int Tw = 0;
+        int Tw = 0, Tmin = 1 << 30;
         for (int u = 0; u < U; ++u) {
             const long long s = w * U + u;
             if (s < R) {
                 slen[(size_t)s] = len[(size_t)perm[(size_t)s]];
                 sseq[(size_t)s] = (int)perm[(size_t)s];
                 Tw = std::max(Tw, slen[(size_t)s]);
+                Tmin = std::min(Tmin, slen[(size_t)s]);
             }
         }
         const long long nch = (Tw + kChunk - 1) / kChunk;
         wT[(size_t)w] = Tw;
+        wfull[(size_t)w] = (Tmin == Tw) ? 1 : 0;
         wsym[(size_t)w] = symtot;
-        waoff[(size_t)w] = atot;
-        weoff[(size_t)w] = etot;
+        wck[(size_t)w] = cktot;
+        wsp[(size_t)w] = sptot;
         symtot += nch * U * kChunk;
-        atot += nch * kChunk * kWave;
-        etot += (nch * kChunk + kChunk) * U;
+        if (c->wide) {  // full alpha_hat [t][64] + exponents [t] (+1 chunk)
+            cktot += nch * kChunk * kWave;
+            sptot += nch * kChunk + kChunk;
+        } else {        // one checkpoint per chunk [c][64] + exponent packs [c][u]
+            cktot += nch * kWave;
+            sptot += nch * U;
+        }
     }
+    // packs hold LDS byte offsets of the emission rows when the tables live in LDS (< 48 KiB, so
+    // they fit uint16), symbol ids otherwise
+    const bool lds_off = c->lds_tables();
+    const long long row_bytes = (long long)(c->G + 1) * (long long)sizeof(double);
     std::vector<uint16_t> hsym((size_t)std::max(symtot, 1LL), 0);
     for (long long w = 0; w < nwaves; ++w)
         for (int u = 0; u < U; ++u) {
@@ -1092,38 +1384,66 @@ int hmmbw_set_observations(hmmbw_ctx *c, const int64_t *offsets, const int32_t *
             const int T = len[(size_t)r];
             for (int t = 0; t < T; ++t)
                 hsym[(size_t)(wsym[(size_t)w] + ((long long)(t / kChunk) * U + u) * kChunk + t % kChunk)] =
-                    (uint16_t)symbols[offsets[r] + t];
+                    (uint16_t)(lds_off ? symbols[offsets[r] + t] * row_bytes : symbols[offsets[r] + t]);
         }
-    dfree(c->d_sym); dfree(c->d_wsym); dfree(c->d_waoff); dfree(c->d_weoff);
-    dfree(c->d_wT); dfree(c->d_slen); dfree(c->d_sseq);
-    dfree(c->d_alpha); dfree(c->d_logp); dfree(c->d_ebuf);
-    c->has_obs = false;
+    free_obs(c);
+    const int wpb = kBlock / kWave;
+    const long long nblocks = (nwaves + wpb - 1) / wpb;
     int rc = dalloc(&c->d_sym, (size_t)std::max(symtot, 1LL));
     if (!rc) rc = dalloc(&c->d_wsym, (size_t)nwaves);
-    if (!rc) rc = dalloc(&c->d_waoff, (size_t)nwaves);
-    if (!rc) rc = dalloc(&c->d_weoff, (size_t)nwaves);
+    if (!rc) rc = dalloc(&c->d_wckoff, (size_t)nwaves);
+    if (!rc) rc = dalloc(&c->d_wspoff, (size_t)nwaves);
     if (!rc) rc = dalloc(&c->d_wT, (size_t)nwaves);
+    if (!rc) rc = dalloc(&c->d_wfull, (size_t)nwaves);
     if (!rc) rc = dalloc(&c->d_slen, (size_t)(nwaves * U));
     if (!rc) rc = dalloc(&c->d_sseq, (size_t)(nwaves * U));
-    if (!rc) rc = dalloc(&c->d_alpha, (size_t)std::max(atot, 1LL));
-    if (!rc) rc = dalloc(&c->d_ebuf, (size_t)std::max(etot, 1LL));
+    if (!rc) rc = dalloc(&c->d_ck, (size_t)std::max(cktot, 1LL));
+    if (!rc) {
+        if (c->wide) rc = dalloc(&c->d_ebuf, (size_t)std::max(sptot, 1LL));
+        else rc = dalloc(&c->d_sp, (size_t)std::max(sptot, 1LL));
+    }
     if (!rc) rc = dalloc(&c->d_logp, (size_t)std::max<int64_t>(R, 1));
+    if (!rc) rc = dalloc(&c->d_llpart, 2 * (size_t)std::max(nblocks, 1LL));
     if (rc) return rc;
     HIP_TRY(hipMemcpy(c->d_sym, hsym.data(), sizeof(uint16_t) * hsym.size(), hipMemcpyHostToDevice));
     if (nwaves > 0) {
         HIP_TRY(hipMemcpy(c->d_wsym, wsym.data(), sizeof(long long) * nwaves, hipMemcpyHostToDevice));
-        HIP_TRY(hipMemcpy(c->d_waoff, waoff.data(), sizeof(long long) * nwaves, hipMemcpyHostToDevice));
-        HIP_TRY(hipMemcpy(c->d_weoff, weoff.data(), sizeof(long long) * nwaves, hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(c->d_wckoff, wck.data(), sizeof(long long) * nwaves, hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(c->d_wspoff, wsp.data(), sizeof(long long) * nwaves, hipMemcpyHostToDevice));
         HIP_TRY(hipMemcpy(c->d_wT, wT.data(), sizeof(int) * nwaves, hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(c->d_wfull, wfull.data(), sizeof(int) * nwaves, hipMemcpyHostToDevice));
         HIP_TRY(hipMemcpy(c->d_slen, slen.data(), sizeof(int) * nwaves * U, hipMemcpyHostToDevice));
         HIP_TRY(hipMemcpy(c->d_sseq, sseq.data(), sizeof(int) * nwaves * U, hipMemcpyHostToDevice));
     }
     std::vector<double> ninf((size_t)std::max<int64_t>(R, 1), -INFINITY);
     HIP_TRY(hipMemcpy(c->d_logp, ninf.data(), sizeof(double) * ninf.size(), hipMemcpyHostToDevice));
+    std::vector<double> zpairs(2 * (size_t)std::max(nblocks, 1LL), 0.0);
+    HIP_TRY(hipMemcpy(c->d_llpart, zpairs.data(), sizeof(double) * zpairs.size(), hipMemcpyHostToDevice));
     c->R = R;
     c->nwaves = nwaves;
+    c->nblocks = nblocks;
     c->has_obs = true;
     return HMMBW_OK;
+}
+
+int hmmbw_set_option(hmmbw_ctx *c, int key, int64_t value) {
+    if (!c) return fail(HMMBW_E_INVALID, "null context");
+    if (key == HMMBW_OPT_SAFE_SCALING) {
+        c->force_safe = value != 0;
+        return HMMBW_OK;
+    }
+    if (key == HMMBW_OPT_STAT_COPIES) {
+        if (value < 1 || value > 1024) return fail(HMMBW_E_INVALID, "statistics copies must be in [1, 1024]");
+        if (int rc = set_device(c)) return rc;
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        c->ncopies = (int)value;
+        return realloc_stats(c);
+    }
+    if (key == HMMBW_OPT_ABLATE) {  // diagnostics: results are wrong while set
+        c->ablate = (int)value;
+        return HMMBW_OK;
+    }
+    return fail(HMMBW_E_INVALID, "unknown option " + std::to_string(key));
 }
 
 int hmmbw_set_params(hmmbw_ctx *c, const double *pi, const double *A, const double *B) {
@@ -1133,7 +1453,7 @@ int hmmbw_set_params(hmmbw_ctx *c, const double *pi, const double *A, const doub
     const int N = c->N, K = c->K, G = c->G;
     // safe_log semantics (hmm_training.py:46-54): x <= 0 (and NaN) is a zero probability
     auto clean = [](double x) { return x > 0.0 ? x : 0.0; };
-    std::vector<double> hpi(N), hA((size_t)N * N), hB((size_t)N * K), hBt((size_t)K * G, 0.0);
+    std::vector<double> hpi(N), hA((size_t)N * N), hB((size_t)N * K), hBt((size_t)K * G + G, 0.0);
     for (int i = 0; i < N; ++i) hpi[i] = clean(pi[i]);
     for (size_t i = 0; i < hA.size(); ++i) hA[i] = clean(A[i]);
     for (int jj = 0; jj < N; ++jj)
@@ -1157,7 +1477,7 @@ int hmmbw_reset_training(hmmbw_ctx *c, double epsilon, int64_t max_iterations) {
     if (int rc = set_device(c)) return rc;
     hipLaunchKernelGGL(k_init_state, dim3(1), dim3(1), 0, c->stream, c->d_state, epsilon, (long long)max_iterations);
     HIP_TRY(hipGetLastError());
-    HIP_TRY(hipMemsetAsync(c->d_stats, 0, sizeof(double) * c->stats_len(), c->stream));
+    HIP_TRY(hipMemsetAsync(c->d_copies, 0, sizeof(double) * c->ncopies * c->copy_len(), c->stream));
     c->armed = true;
     return HMMBW_OK;
 }
@@ -1171,9 +1491,11 @@ int hmmbw_stats_len(const hmmbw_ctx *c, int64_t *n) {
 int hmmbw_estep(hmmbw_ctx *c, double *stats_dev) {
     if (int rc = check_ready(c, true)) return rc;
     if (!stats_dev) return fail(HMMBW_E_INVALID, "null stats buffer");
-    if (int rc = launch_estep(c, stats_dev, false, c->d_state)) return rc;
-    hipLaunchKernelGGL(k_seq_lse, dim3(1), dim3(1024), 0, c->stream, c->d_logp, c->R, stats_dev, c->off_ll(),
-                       c->rank, c->d_state);
+    if (int rc = launch_estep(c, false, c->d_state)) return rc;
+    const long long n = c->copy_len();
+    const unsigned grid = (unsigned)std::min<long long>((n + 255) / 256, 64);
+    hipLaunchKernelGGL(k_reduce_local, dim3(grid), dim3(256), 0, c->stream, c->d_copies, c->ncopies, n, c->d_llpart,
+                       c->nblocks, stats_dev, c->off_ll(), c->world, c->rank, c->d_state);
     HIP_TRY(hipGetLastError());
     return HMMBW_OK;
 }
@@ -1188,8 +1510,8 @@ int hmmbw_iterate(hmmbw_ctx *c, int64_t n_iter) {
     if (int rc = check_ready(c, true)) return rc;
     if (c->world != 1) return fail(HMMBW_E_STATE, "hmmbw_iterate is single-rank; use estep/all-reduce/mstep");
     for (int64_t i = 0; i < n_iter; ++i) {
-        if (int rc = launch_estep(c, c->d_stats, false, c->d_state)) return rc;
-        if (int rc = launch_mstep(c, c->d_stats, c->R, true)) return rc;
+        if (int rc = launch_estep(c, false, c->d_state)) return rc;
+        if (int rc = launch_mstep(c, nullptr, c->R, true)) return rc;
         if (c->timing && c->ev_pending.size() >= 256)
             if (int rc = drain_timing(c)) return rc;
     }
@@ -1255,7 +1577,7 @@ int hmmbw_get_loglik(hmmbw_ctx *c, double *out) {
 int hmmbw_score(hmmbw_ctx *c, double *out) {
     if (int rc = check_ready(c, false)) return rc;
     if (!out) return fail(HMMBW_E_INVALID, "null argument");
-    if (int rc = launch_estep(c, c->d_stats, true, nullptr)) return rc;
+    if (int rc = launch_estep(c, true, nullptr)) return rc;
     return hmmbw_get_loglik(c, out);
 }
 

@@ -18,7 +18,7 @@ from typing import Callable, List, Optional, Sequence, Tuple
 import numpy as np
 import torch
 
-from ._lib import TOPOLOGY, TOPOLOGY_NAME, IterRecord, Status, check, lib
+from ._lib import OPT_SAFE_SCALING, TOPOLOGY, TOPOLOGY_NAME, IterRecord, Status, check, lib
 
 IterCallback = Callable[[int, float, float], None]
 
@@ -104,7 +104,7 @@ class BaumWelchEngine:
     """Baum-Welch training / scoring of one discrete HMM (N states, M symbols) on one GPU."""
 
     def __init__(self, n_states: int, n_symbols: int, device: Optional[int] = None, topology: str = "auto",
-                 rank: int = 0, world_size: int = 1, stream: Optional[int] = None):
+                 rank: int = 0, world_size: int = 1, stream: Optional[int] = None, safe_scaling: bool = False):
         self._lib = lib()
         self.N, self.M = int(n_states), int(n_symbols)
         self.device = default_device() if device is None else int(device)
@@ -119,6 +119,8 @@ class BaumWelchEngine:
         if self.world_size > 1:
             check(self._lib.hmmbw_set_rank(self._ctx, self.rank, self.world_size))
         check(self._lib.hmmbw_set_topology(self._ctx, TOPOLOGY[topology]))
+        if safe_scaling:
+            check(self._lib.hmmbw_set_option(self._ctx, OPT_SAFE_SCALING, 1))
         self.n_seq = 0
         self.n_seq_global = 0
 

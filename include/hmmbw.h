@@ -93,10 +93,11 @@ int hmmbw_reset_training(hmmbw_ctx *ctx, double epsilon, int64_t max_iterations)
 /* Length (in doubles) of the packed sufficient-statistics buffer used by estep/mstep. */
 int hmmbw_stats_len(const hmmbw_ctx *ctx, int64_t *n_doubles);
 
-/* E-step over this rank's sequences (hmm_training.py:351-410): accumulates the packed statistics
+/* E-step over this rank's sequences (hmm_training.py:351-410): writes this rank's packed statistics
  * {pi_num[N], S[N*N], gamma_den_excl_last[N], gamma_den_all[N], B_num[M*N], (m, s)[world]}
- * into the zero-filled DEVICE buffer stats_dev and writes this rank's (max, sum-exp) pair of
- * log P_r into its slot.  Multi-rank callers all-reduce(sum) stats_dev, then call hmmbw_mstep. */
+ * into the DEVICE buffer stats_dev (hmmbw_stats_len doubles; its (m, s) pair — the max and
+ * sum-exp of log P_r — in slot `rank`, other slots zero).  Multi-rank callers all-reduce(sum)
+ * stats_dev, then call hmmbw_mstep. */
 int hmmbw_estep(hmmbw_ctx *ctx, double *stats_dev);
 
 /* M-step + convergence (hmm_training.py:415-514) from the (all-reduced) statistics; n_seq_global
@@ -122,6 +123,18 @@ int hmmbw_get_loglik(hmmbw_ctx *ctx, double *out);
 /* SYNC. Forward-only scoring of the loaded sequences under the current parameters:
  * hmm_testing.py:49-104 calculate_log_likelihood for every sequence, one launch. */
 int hmmbw_score(hmmbw_ctx *ctx, double *out);
+
+/* Engine knobs.  HMMBW_OPT_SAFE_SCALING = 1 forces the per-step power-of-two normalisation of the
+ * forward recursion (default 0: lagged normalisation, automatic per-wave fallback to the per-step
+ * form when magnitudes leave [2^-900, 2^900]).  Results agree to fp64 rounding either way. */
+#define HMMBW_OPT_SAFE_SCALING 1
+/* Diagnostics only (profiling ablations; results are WRONG while nonzero): bit 0 skips the E-step's
+ * statistics flush, bit 1 skips its backward sweep. */
+#define HMMBW_OPT_ABLATE 2
+/* Number of statistics accumulator copies the E-step's workgroups spread their atomics over
+ * (workgroup b adds into copy b % n; default 1). */
+#define HMMBW_OPT_STAT_COPIES 3
+int hmmbw_set_option(hmmbw_ctx *ctx, int key, int64_t value);
 
 /* E-step kernel timing with HIP events on the context stream (for bench/roofline). */
 int hmmbw_timing(hmmbw_ctx *ctx, int enable, double *total_ms, int64_t *count);

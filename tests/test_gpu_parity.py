@@ -133,14 +133,20 @@ SWEEP += [(8, 700, "dense"), (8, 700, "left_to_right"), (16, 300, "dense"), (17,
           (33, 64, "dense"), (64, 300, "dense")]
 
 
+SAFE_SWEEP = [(N, K, topo) for (N, K, topo) in SWEEP if N in (2, 5, 8, 16)]
+
+
+@pytest.mark.parametrize("safe", [False, True])
 @pytest.mark.parametrize("N,K,topology", SWEEP)
-def test_training_vs_oracle_random(N, K, topology, oracle):
+def test_training_vs_oracle_random(N, K, topology, safe, oracle):
     from hmm_training_amd.engine import BaumWelchEngine, to_csr
+    if safe and (N, K, topology) not in SAFE_SWEEP:
+        pytest.skip("safe-scaling mode swept on a subset")
     rng = np.random.default_rng(1000 * N + K)
     obs, pi, A, B = random_problem(rng, N, K, R=37, tmax=90, topology=topology)
     off, sym = to_csr(obs)
     ref = oracle.hmm_training(off, sym.astype(np.int64), N, K, 1e-6, 3, pi, A, B)
-    with BaumWelchEngine(N, K, topology=topology) as eng:
+    with BaumWelchEngine(N, K, topology=topology, safe_scaling=safe) as eng:
         eng.set_observations(obs)
         eng.set_params(pi, A, B)
         assert eng.topology == topology
@@ -266,3 +272,34 @@ def test_score_matrix_and_timing():
         eng.enqueue_iterations(4)
         ms, n = eng.timing(0)
         assert n == 4 and ms > 0
+
+
+@pytest.mark.parametrize("topology", ["left_to_right", "dense"])
+@pytest.mark.parametrize("equal_lengths", [True, False])
+def test_pathological_emissions_fall_back_to_safe_scaling(topology, equal_lengths, oracle):
+    """A symbol with probability 1e-200 in every state collapses the lagged scaling; the kernel must
+    detect it and redo the wave with per-step normalisation, matching the log-domain oracle."""
+    from hmm_training_amd.engine import BaumWelchEngine, to_csr
+    rng = np.random.default_rng(99)
+    N, K = 8, 32
+    obs, pi, A, B = random_problem(rng, N, K, R=24, tmax=60, topology=topology)
+    if equal_lengths:
+        obs = [rng.integers(0, K, size=60) for _ in range(24)]
+    B[:, 3] = 1e-200
+    B /= B.sum(1, keepdims=True)
+    for o in obs:
+        o[::4] = 3  # frequent, nearly impossible symbol
+    off, sym = to_csr(obs)
+    ref = oracle.hmm_training(off, sym.astype(np.int64), N, K, 1e-6, 2, pi, A, B)
+    assert np.all(np.isfinite(ref.logP))
+    with BaumWelchEngine(N, K, topology=topology) as eng:
+        eng.set_observations(obs)
+        eng.set_params(pi, A, B)
+        trace = []
+        eng.train(1e-6, 2, lambda k, L, df: trace.append(L))
+        assert_ll(trace, ref.trace_L)
+        assert_ll(eng.loglik(), ref.logP)
+        p2, A2, B2 = eng.params(normalise=True)
+    assert_params(A2, ref.A, "A")
+    assert_params(B2, ref.B, "B")
+    assert_params(p2, ref.pi, "pi")
