@@ -39,8 +39,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level para
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=20)
-    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--R", type=int, default=10_000, help="sequences per GPU")
     p.add_argument("--T", type=int, default=200)
     p.add_argument("--N", type=int, default=8)
@@ -49,6 +49,8 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline sample budget")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--seed", type=int, default=3)
+    p.add_argument("--no-kernel-timing", action="store_true", help="skip the HIP events")
+    p.add_argument("--timing-every", type=int, default=5, help="time every k-th E-step launch")
     return p.parse_args()
 
 
@@ -132,7 +134,7 @@ def main():
 
     eng.enqueue_iterations(args.warmup, stats)
     torch.cuda.synchronize()
-    eng.timing(1)
+    eng.timing(0 if args.no_kernel_timing else args.timing_every)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -156,7 +158,7 @@ def main():
     value = R * world * args.steps / elapsed
     kern_s = kern_ms / max(kern_n, 1) / 1000.0
     bu = bytes_per_sequence(T, N)
-    achieved = bu * R / kern_s / 1e9
+    achieved = bu * R / kern_s / 1e9 if kern_s > 0 else float("nan")
     cfg_key = f"R{R}_T{T}_N{N}_K{K}_{args.topology}"
     traffic = find_traffic(cfg_key)
 

@@ -36,6 +36,9 @@ EXPORTED = (
     "hmmbw_set_option",
 )
 OPT_SAFE_SCALING = 1
+OPT_ABLATE = 2
+OPT_STAT_COPIES = 3
+OPT_FUSE_MSTEP = 4
 
 
 class HMMBWError(RuntimeError):

@@ -78,6 +78,22 @@ struct Layout {
     long long nwaves;
 };
 
+struct MArgs {
+    const double *src;     // statistics: the copies (single rank) or the all-reduced buffer
+    double *zero_ll;       // LL slots to clear (multi-rank) or nullptr
+    int nsrc;
+    long long copy_len;
+    double *pi, *A, *B, *Bt;
+    const double *llpart;
+    long long nblocks;
+    long long R_global;
+    IterState *state;
+    double *hist;
+    int N, K, G, world;
+    int local_lse;
+    long long off_S, off_gex, off_gall, off_bnum, off_ll;
+};
+
 struct EArgs {
     Layout L;
     const double *pi;
@@ -96,6 +112,9 @@ struct EArgs {
     int N;
     int force_safe;    // 1: per-step normalisation (no lagged scaling)
     int ablate;        // diagnostics only: bit 0 skips the statistics flush, bit 1 the backward sweep
+    int fused;         // 1: the last workgroup to finish runs the M-step (single rank)
+    unsigned *ticket;  // workgroup completion counter for the fused M-step
+    MArgs m;
     long long off_S, off_gex, off_gall, off_bnum;
 };
 
@@ -208,8 +227,9 @@ __device__ void block_ll_partial(double lp, bool valid, double *sh, double *out)
     if (tid == 0) {
         double S = 0.0;
         for (int w = 0; w < nw; ++w) S += sh[w];
-        out[0] = (S > 0.0) ? M : 0.0;
-        out[1] = S;
+        // memory-side atomics: the fused M-step of the last workgroup reads these with atomics too
+        atomicExch(&out[0], (S > 0.0) ? M : 0.0);
+        atomicExch(&out[1], S);
     }
 }
 
@@ -231,6 +251,8 @@ __device__ void block_ll_partial(double lp, bool valid, double *sh, double *out)
 //   gamma_t(i) = z_t(i) beta_hat_t(i),  xi_t(i,j) = a_ij z_t(i) v_j  (accumulated as S_ij = xi/a_ij).
 // gamma is scattered into the per-workgroup LDS histogram B_num[o_t][j] (ds_add_f64).
 // ---------------------------------------------------------------------------------------------
+__device__ void estep_tail(const EArgs &a, double *lds);
+
 template <int N, int G, bool LR, bool LDSTAB, bool FWD_ONLY>
 __global__ void __launch_bounds__(kBlock) k_estep_small(EArgs a) {
     constexpr int U = kWave / G;
@@ -599,6 +621,8 @@ __global__ void __launch_bounds__(kBlock) k_estep_small(EArgs a) {
             }
         }
     }
+    if constexpr (!FWD_ONLY)
+        if (a.fused) estep_tail(a, smem);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -765,16 +789,25 @@ __device__ double block_reduce(double x, double *sh, bool is_max) {
 }
 
 // Combine per-block (max, sum exp) pairs into this rank's pair (log_sum_exp :66-79 over :503).
+// ATOMIC: read with returning memory-side atomics (inside the producing kernel, where the per-XCD
+// L2s give no cross-workgroup visibility for plain loads).
+template <bool ATOMIC = false>
+__device__ __forceinline__ double rd(const double *p) {
+    if constexpr (ATOMIC) return unsafeAtomicAdd(const_cast<double *>(p), 0.0);
+    else return *p;
+}
+
+template <bool ATOMIC = false>
 __device__ void combine_ll_pairs(const double *pairs, long long n, double *sh, double *m_out, double *s_out) {
     double mx = -INFINITY;
     for (long long r = threadIdx.x; r < n; r += blockDim.x)
-        if (pairs[2 * r + 1] > 0.0) mx = fmax(mx, pairs[2 * r]);
+        if (rd<ATOMIC>(&pairs[2 * r + 1]) > 0.0) mx = fmax(mx, rd<ATOMIC>(&pairs[2 * r]));
     mx = block_reduce(mx, sh, true);
     double s = 0.0;
     if (mx != -INFINITY)
         for (long long r = threadIdx.x; r < n; r += blockDim.x) {
-            const double sr = pairs[2 * r + 1];
-            if (sr > 0.0) s += sr * exp(pairs[2 * r] - mx);
+            const double sr = rd<ATOMIC>(&pairs[2 * r + 1]);
+            if (sr > 0.0) s += sr * exp(rd<ATOMIC>(&pairs[2 * r]) - mx);
         }
     s = block_reduce(s, sh, false);
     *m_out = mx;
@@ -810,44 +843,35 @@ __global__ void __launch_bounds__(256) k_reduce_local(double *copies, int ncopie
     }
 }
 
-struct MArgs {
-    const double *src;     // statistics: the copies (single rank) or the all-reduced buffer
-    double *zero_ll;       // LL slots to clear (multi-rank) or nullptr
-    int nsrc;
-    long long copy_len;
-    double *pi, *A, *B, *Bt;
-    const double *llpart;
-    long long nblocks;
-    long long R_global;
-    IterState *state;
-    double *hist;
-    int N, K, G, world;
-    int local_lse;
-    long long off_S, off_gex, off_gall, off_bnum, off_ll;
-};
 
 // sum of one statistic over the copies, clearing them for the next iteration
+template <bool ATOMIC>
 __device__ __forceinline__ double take(const MArgs &m, long long idx) {
     double v = 0.0;
     double *p = const_cast<double *>(m.src) + idx;
     for (int c = 0; c < m.nsrc; ++c) {
-        v += p[c * m.copy_len];
-        p[c * m.copy_len] = 0.0;
+        if constexpr (ATOMIC) {
+            v += atomicExch(p + c * m.copy_len, 0.0);
+        } else {
+            v += p[c * m.copy_len];
+            p[c * m.copy_len] = 0.0;
+        }
     }
     return v;
 }
 
-__global__ void __launch_bounds__(256) k_mstep(MArgs m) {
+// M-step + convergence by one workgroup of 256 threads (hmm_training.py:415-514).
+template <bool ATOMIC>
+__device__ void mstep_block(const MArgs &m) {
     __shared__ double sh[16];
     __shared__ double sL;
     __shared__ double sPi[64], sGex[64], sGall[64];
     IterState *st = m.state;
-    if (st->done) return;
     const int tid = threadIdx.x;
     // L = LSE_r log P_r over all ranks (:503)
     if (m.local_lse) {
         double mx, s;
-        combine_ll_pairs(m.llpart, m.nblocks, sh, &mx, &s);
+        combine_ll_pairs<ATOMIC>(m.llpart, m.nblocks, sh, &mx, &s);
         if (tid == 0) sL = (s > 0.0) ? mx + log(s) : -INFINITY;
     } else if (tid == 0) {
         const double *ll = m.src + m.off_ll;
@@ -863,9 +887,9 @@ __global__ void __launch_bounds__(256) k_mstep(MArgs m) {
     }
     const int N = m.N, K = m.K;
     for (int i = tid; i < N; i += blockDim.x) {
-        sPi[i] = take(m, i);
-        sGex[i] = take(m, m.off_gex + i);
-        sGall[i] = take(m, m.off_gall + i);
+        sPi[i] = take<ATOMIC>(m, i);
+        sGex[i] = take<ATOMIC>(m, m.off_gex + i);
+        sGall[i] = take<ATOMIC>(m, m.off_gall + i);
     }
     __syncthreads();
     // pi (:415-424): LSE_r gamma_0 - log R ; no term -> -inf
@@ -873,14 +897,14 @@ __global__ void __launch_bounds__(256) k_mstep(MArgs m) {
     // A (:429-455): xi numerator = a_ij * S_ij ; denominator excludes the last frame
     for (int idx = tid; idx < N * N; idx += blockDim.x) {
         const double den = sGex[idx / N];
-        const double num = m.A[idx] * take(m, m.off_S + idx);
+        const double num = m.A[idx] * take<ATOMIC>(m, m.off_S + idx);
         m.A[idx] = (den > 0.0 && num > 0.0) ? num / den : 0.0;
     }
     // B (:460-497): floor 1e-20 when no gamma term carries the symbol; empty denominator -> row 0
     for (long long idx = tid; idx < (long long)N * K; idx += blockDim.x) {
         const int jj = (int)(idx % N), k = (int)(idx / N);  // symbol-major: coalesced over the copies
         const double den = sGall[jj];
-        const double num = take(m, m.off_bnum + idx);
+        const double num = take<ATOMIC>(m, m.off_bnum + idx);
         const double v = den > 0.0 ? (num > 0.0 ? num / den : 1e-20) : 0.0;
         m.B[(long long)jj * K + k] = v;
         m.Bt[(long long)k * m.G + jj] = v;
@@ -903,6 +927,162 @@ __global__ void __launch_bounds__(256) k_mstep(MArgs m) {
             st->converged = (it + 1 < st->max_iterations) ? 1 : 0;
         }
     }
+}
+
+__global__ void __launch_bounds__(256) k_mstep(MArgs m) {
+    if (m.state->done) return;
+    mstep_block<false>(m);
+}
+
+
+// merge (max, sum exp) pairs: online log-sum-exp
+__device__ __forceinline__ void ll_merge(double &M, double &S, double m2, double s2) {
+    if (!(s2 > 0.0)) return;
+    if (!(S > 0.0)) { M = m2; S = s2; return; }
+    if (m2 > M) { S = S * exp(M - m2) + s2; M = m2; }
+    else S += s2 * exp(m2 - M);
+}
+
+// M-step staged through LDS (sSt: copy_len doubles): the statistics (summed over the copies, which
+// are cleared) and the per-workgroup log-likelihood pairs are gathered in independent batches, then
+// the update runs from LDS.  ATOMIC (fused into the E-step): gathered with returning memory-side
+// atomics; otherwise (its own kernel, after a kernel boundary) with plain loads.
+template <bool ATOMIC>
+__device__ void mstep_staged(const MArgs &m, double *sSt) {
+    __shared__ double sM[16], sS[16];
+    __shared__ double sL;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, nw = blockDim.x >> 6;
+    const int N = m.N, K = m.K;
+    const long long len = m.copy_len;
+    // ---- one batch of independent loads: old A, convergence state, LL pairs, statistics ----
+    const double a_old = tid < N * N ? m.A[tid] : 0.0;  // N*N <= 256 for the staged path
+    double prev = 0.0, eps = 0.0;
+    long long it = 0, maxit = 0;
+    if (tid == 0) {
+        prev = m.state->prev_L;
+        eps = m.state->epsilon;
+        it = m.state->iteration;
+        maxit = m.state->max_iterations;
+    }
+    // Branch-free, clamped addresses so the compiler issues every load of a batch before the first
+    // wait (a guarded load inside a runtime loop serialises on its own s_waitcnt).
+    constexpr int PB = 4;
+    double pm[PB], ps[PB];
+    double M = -INFINITY, S = 0.0;
+    const long long nb = m.nblocks;
+    for (long long r0 = 0; r0 < nb; r0 += (long long)PB * blockDim.x) {
+#pragma unroll
+        for (int u = 0; u < PB; ++u) {
+            const long long r = r0 + (long long)u * blockDim.x + tid;
+            const long long rc = r < nb ? r : nb - 1;
+            pm[u] = rd<ATOMIC>(m.llpart + 2 * rc);
+            ps[u] = rd<ATOMIC>(m.llpart + 2 * rc + 1);
+        }
+#pragma unroll
+        for (int u = 0; u < PB; ++u) {
+            const bool ok = r0 + (long long)u * blockDim.x + tid < nb;
+            ll_merge(M, S, ok ? pm[u] : -INFINITY, ok ? ps[u] : 0.0);
+        }
+    }
+    constexpr int B = 16;
+    double *src = const_cast<double *>(m.src);
+    for (long long base = 0; base < len; base += (long long)B * blockDim.x) {
+        double v[B];
+#pragma unroll
+        for (int u = 0; u < B; ++u) v[u] = 0.0;
+        for (int c = 0; c < m.nsrc; ++c) {
+            double x[B];
+#pragma unroll
+            for (int u = 0; u < B; ++u) {
+                const long long idx = base + (long long)u * blockDim.x + tid;
+                double *q = src + c * len + (idx < len ? idx : len - 1);
+                if constexpr (ATOMIC) x[u] = idx < len ? atomicExch(q, 0.0) : 0.0;
+                else x[u] = *q;
+            }
+#pragma unroll
+            for (int u = 0; u < B; ++u) v[u] += x[u];
+        }
+#pragma unroll
+        for (int u = 0; u < B; ++u) {
+            const long long idx = base + (long long)u * blockDim.x + tid;
+            if (idx < len) {
+                sSt[idx] = v[u];
+                if constexpr (!ATOMIC)
+                    for (int c = 0; c < m.nsrc; ++c) src[c * len + idx] = 0.0;
+            }
+        }
+    }
+    // ---- L = LSE_r log P_r (:503) ----
+    for (int k = 32; k >= 1; k >>= 1) ll_merge(M, S, __shfl_xor(M, k), __shfl_xor(S, k));
+    if (lane == 0) { sM[wv] = M; sS[wv] = S; }
+    __syncthreads();
+    if (tid == 0) {
+        double MM = -INFINITY, SS = 0.0;
+        for (int w = 0; w < nw; ++w) ll_merge(MM, SS, sM[w], sS[w]);
+        sL = (SS > 0.0) ? MM + log(SS) : -INFINITY;
+    }
+    __syncthreads();
+    const double *sPi = sSt, *sS_ = sSt + m.off_S, *sGex = sSt + m.off_gex, *sGall = sSt + m.off_gall,
+                 *sBn = sSt + m.off_bnum;
+    // pi (:415-424), A (:429-455), B (:460-497)
+    if (tid < N) m.pi[tid] = sPi[tid] > 0.0 ? sPi[tid] / (double)m.R_global : 0.0;
+    if (tid < N * N) {
+        const double den = sGex[tid / N];
+        const double num = a_old * sS_[tid];
+        m.A[tid] = (den > 0.0 && num > 0.0) ? num / den : 0.0;
+    }
+    for (int idx = tid; idx < N * K; idx += blockDim.x) {
+        const int k = idx / N, jj = idx - k * N;
+        const double den = sGall[jj];
+        const double num = sBn[idx];
+        const double v = den > 0.0 ? (num > 0.0 ? num / den : 1e-20) : 0.0;
+        m.B[(long long)jj * K + k] = v;
+        m.Bt[(long long)k * m.G + jj] = v;
+    }
+    if (tid == 0) {
+        IterState *st = m.state;
+        const double L = sL;
+        const double diff = (prev != -INFINITY) ? fabs(L - prev) : INFINITY;  // :505-508
+        m.hist[2 * (it % kHist)] = L;
+        m.hist[2 * (it % kHist) + 1] = diff;
+        st->prev_L = L;
+        st->last_L = L;
+        st->last_diff = diff;
+        st->iteration = it + 1;
+        const bool cont = (diff >= eps) && (it + 1 < maxit);  // :346
+        if (!cont) {
+            st->done = 1;
+            st->converged = (it + 1 < maxit) ? 1 : 0;
+        }
+    }
+}
+
+// single-rank M-step with the statistics staged in dynamic LDS (copy_len doubles)
+__global__ void __launch_bounds__(256) k_mstep_staged(MArgs m) {
+    extern __shared__ double sSt[];
+    if (m.state->done) return;
+    mstep_staged<false>(m, sSt);
+}
+
+// Fused M-step: the last E-step workgroup to finish (completion ticket) runs it.  Every value that
+// crosses workgroups inside the kernel (statistics copies, log-likelihood pairs, the ticket) moves
+// through memory-side atomics, so no per-XCD L2 can serve a stale line.
+__device__ void estep_tail(const EArgs &a, double *lds) {
+    __shared__ int last;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's atomics have completed
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        last = atomicAdd(a.ticket, 1u) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!last) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    mstep_staged<true>(a.m, lds);
+    if (threadIdx.x == 0) atomicExch(a.ticket, 0u);
 }
 
 // safe_exp + normalisation of the returned parameters (:524-541)
@@ -1014,7 +1194,9 @@ struct hmmbw_ctx {
     IterState *d_state = nullptr;
     double *d_hist = nullptr;
     double *d_copies = nullptr;   // [ncopies][copy_len] E-step accumulators
+    unsigned *d_ticket = nullptr; // fused M-step completion counter
     int ncopies = 1;
+    bool fuse_mstep = false;
     bool armed = false;
     // observations
     long long R = 0, nwaves = 0;
@@ -1029,7 +1211,8 @@ struct hmmbw_ctx {
     int force_safe = 0;
     int ablate = 0;
     // timing
-    bool timing = false;
+    int timing = 0;              // 0: off; k >= 1: time every k-th E-step launch
+    long long timing_seq = 0;
     std::vector<hipEvent_t> ev_free, ev_pending;  // pairs (start, stop)
     double timed_ms = 0.0;
     long long timed_n = 0;
@@ -1094,6 +1277,45 @@ EArgs make_eargs(hmmbw_ctx *c) {
     return a;
 }
 
+// local: the statistics are this context's copies; otherwise the caller's all-reduced buffer
+MArgs make_margs(hmmbw_ctx *c, double *stats, long long R_global, bool local) {
+    MArgs m{};
+    m.src = local ? c->d_copies : stats;
+    m.zero_ll = local ? nullptr : stats + c->off_ll();
+    m.nsrc = local ? c->ncopies : 1;
+    m.copy_len = c->copy_len();
+    m.pi = c->d_pi;
+    m.A = c->d_A;
+    m.B = c->d_B;
+    m.Bt = c->d_Bt;
+    m.llpart = c->d_llpart;
+    m.nblocks = c->nblocks;
+    m.R_global = R_global;
+    m.state = c->d_state;
+    m.hist = c->d_hist;
+    m.N = c->N;
+    m.K = c->K;
+    m.G = c->G;
+    m.world = c->world;
+    m.local_lse = local ? 1 : 0;
+    m.off_S = c->off_S();
+    m.off_gex = c->off_gex();
+    m.off_gall = c->off_gall();
+    m.off_bnum = c->off_bnum();
+    m.off_ll = c->off_ll();
+    return m;
+}
+
+int launch_mstep(hmmbw_ctx *c, double *stats, long long R_global, bool local) {
+    const size_t staged = sizeof(double) * (size_t)c->copy_len();
+    if (local && staged <= 64 * 1024 && c->N * c->N <= 256)
+        hipLaunchKernelGGL(k_mstep_staged, dim3(1), dim3(256), staged, c->stream, make_margs(c, stats, R_global, local));
+    else
+        hipLaunchKernelGGL(k_mstep, dim3(1), dim3(256), 0, c->stream, make_margs(c, stats, R_global, local));
+    HIP_TRY(hipGetLastError());
+    return HMMBW_OK;
+}
+
 template <class F>
 int launch_lds(F f, unsigned grid, size_t lds, hipStream_t stream, const EArgs &a) {
     if (lds > 64 * 1024)
@@ -1104,14 +1326,26 @@ int launch_lds(F f, unsigned grid, size_t lds, hipStream_t stream, const EArgs &
     return HMMBW_OK;
 }
 
-int launch_estep(hmmbw_ctx *c, bool fwd_only, const IterState *state) {
+// fuse: ask the last E-step workgroup to run the M-step (single rank); *fused reports whether it will
+int launch_estep(hmmbw_ctx *c, bool fwd_only, const IterState *state, bool fuse = false, bool *fused = nullptr) {
     EArgs a = make_eargs(c);
     a.state = state;
     const int wpb = kBlock / kWave;
     const unsigned grid = (unsigned)((c->nwaves + wpb - 1) / wpb);
+    if (fused) *fused = false;
     if (grid == 0) return HMMBW_OK;
+    const size_t GPh = (size_t)c->G + 1;
+    const size_t lds_small = (c->lds_tables() ? ((size_t)c->K + 1) * GPh + (size_t)c->K * GPh : 0) +
+                             (size_t)wpb * c->G * ((c->topo == HMMBW_TOPOLOGY_LEFT_TO_RIGHT ? 2 : c->N) + 3) + 8;
+    if (fuse && !fwd_only && !c->wide && c->N * c->N <= 256 &&
+        (size_t)c->copy_len() <= std::max<size_t>(lds_small, 8192)) {
+        a.fused = 1;
+        a.ticket = c->d_ticket;
+        a.m = make_margs(c, nullptr, c->R, true);
+        if (fused) *fused = true;
+    }
     hipEvent_t e0 = nullptr, e1 = nullptr;
-    if (c->timing && !fwd_only) {
+    if (c->timing && !fwd_only && (c->timing_seq++ % c->timing) == 0) {
         if (c->ev_free.size() < 2) {
             hipEvent_t x, y;
             HIP_TRY(hipEventCreate(&x));
@@ -1138,7 +1372,8 @@ int launch_estep(hmmbw_ctx *c, bool fwd_only, const IterState *state) {
         const int NV = (lr ? 2 : c->N) + 3;
         const size_t GP = (size_t)c->G + 1;
         const size_t tabs = lds_tab ? ((size_t)c->K + 1) * GP + (fwd_only ? 0 : (size_t)c->K * GP) : 0;
-        const size_t lds = sizeof(double) * (tabs + (size_t)wpb * c->G * NV + 8);
+        size_t lds = sizeof(double) * (tabs + (size_t)wpb * c->G * NV + 8);
+        if (a.fused) lds = std::max(lds, sizeof(double) * (size_t)c->copy_len());  // fused M-step staging
         if (int rc = launch_lds(f, grid, lds, c->stream, a)) return rc;
     }
     if (e1) {
@@ -1160,37 +1395,6 @@ int drain_timing(hmmbw_ctx *c) {
         c->ev_free.push_back(c->ev_pending[i + 1]);
     }
     c->ev_pending.clear();
-    return HMMBW_OK;
-}
-
-// local: the statistics are this context's copies; otherwise the caller's all-reduced buffer
-int launch_mstep(hmmbw_ctx *c, double *stats, long long R_global, bool local) {
-    MArgs m{};
-    m.src = local ? c->d_copies : stats;
-    m.zero_ll = local ? nullptr : stats + c->off_ll();
-    m.nsrc = local ? c->ncopies : 1;
-    m.copy_len = c->copy_len();
-    m.pi = c->d_pi;
-    m.A = c->d_A;
-    m.B = c->d_B;
-    m.Bt = c->d_Bt;
-    m.llpart = c->d_llpart;
-    m.nblocks = c->nblocks;
-    m.R_global = R_global;
-    m.state = c->d_state;
-    m.hist = c->d_hist;
-    m.N = c->N;
-    m.K = c->K;
-    m.G = c->G;
-    m.world = c->world;
-    m.local_lse = local ? 1 : 0;
-    m.off_S = c->off_S();
-    m.off_gex = c->off_gex();
-    m.off_gall = c->off_gall();
-    m.off_bnum = c->off_bnum();
-    m.off_ll = c->off_ll();
-    hipLaunchKernelGGL(k_mstep, dim3(1), dim3(256), 0, c->stream, m);
-    HIP_TRY(hipGetLastError());
     return HMMBW_OK;
 }
 
@@ -1252,6 +1456,8 @@ int hmmbw_ctx_create(int device, int n_states, int n_symbols, hmmbw_ctx **out) {
     if (!rc) rc = dalloc(&c->d_Bt, (size_t)c->K * c->G + c->G);
     if (!rc) rc = dalloc(&c->d_out, (size_t)c->N + (size_t)c->N * c->N + (size_t)c->N * c->K);
     if (!rc) rc = dalloc(&c->d_state, 1);
+    if (!rc) rc = dalloc(&c->d_ticket, 1);
+    if (!rc && hipMemset(c->d_ticket, 0, sizeof(unsigned)) != hipSuccess) rc = fail(HMMBW_E_HIP, "ticket init");
     if (!rc) rc = dalloc(&c->d_hist, 2 * (size_t)kHist);
     if (!rc) rc = realloc_stats(c);
     if (!rc) {
@@ -1273,7 +1479,7 @@ int hmmbw_ctx_destroy(hmmbw_ctx *c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     else (void)hipDeviceSynchronize();
     dfree(c->d_pi); dfree(c->d_A); dfree(c->d_B); dfree(c->d_Bt); dfree(c->d_out);
-    dfree(c->d_state); dfree(c->d_hist); dfree(c->d_copies);
+    dfree(c->d_state); dfree(c->d_hist); dfree(c->d_ticket); dfree(c->d_copies);
     free_obs(c);
     for (auto e : c->ev_free) (void)hipEventDestroy(e);
     for (auto e : c->ev_pending) (void)hipEventDestroy(e);
@@ -1439,6 +1645,10 @@ int hmmbw_set_option(hmmbw_ctx *c, int key, int64_t value) {
         c->ncopies = (int)value;
         return realloc_stats(c);
     }
+    if (key == HMMBW_OPT_FUSE_MSTEP) {
+        c->fuse_mstep = value != 0;
+        return HMMBW_OK;
+    }
     if (key == HMMBW_OPT_ABLATE) {  // diagnostics: results are wrong while set
         c->ablate = (int)value;
         return HMMBW_OK;
@@ -1510,8 +1720,10 @@ int hmmbw_iterate(hmmbw_ctx *c, int64_t n_iter) {
     if (int rc = check_ready(c, true)) return rc;
     if (c->world != 1) return fail(HMMBW_E_STATE, "hmmbw_iterate is single-rank; use estep/all-reduce/mstep");
     for (int64_t i = 0; i < n_iter; ++i) {
-        if (int rc = launch_estep(c, false, c->d_state)) return rc;
-        if (int rc = launch_mstep(c, nullptr, c->R, true)) return rc;
+        bool fused = false;
+        if (int rc = launch_estep(c, false, c->d_state, c->fuse_mstep, &fused)) return rc;
+        if (!fused)
+            if (int rc = launch_mstep(c, nullptr, c->R, true)) return rc;
         if (c->timing && c->ev_pending.size() >= 256)
             if (int rc = drain_timing(c)) return rc;
     }
@@ -1588,7 +1800,8 @@ int hmmbw_timing(hmmbw_ctx *c, int enable, double *total_ms, int64_t *count) {
     if (total_ms) *total_ms = c->timed_ms;
     if (count) *count = c->timed_n;
     if (enable >= 0) {
-        c->timing = enable != 0;
+        c->timing = enable;
+        c->timing_seq = 0;
         c->timed_ms = 0.0;
         c->timed_n = 0;
     }

@@ -18,7 +18,7 @@ from typing import Callable, List, Optional, Sequence, Tuple
 import numpy as np
 import torch
 
-from ._lib import OPT_SAFE_SCALING, TOPOLOGY, TOPOLOGY_NAME, IterRecord, Status, check, lib
+from ._lib import OPT_FUSE_MSTEP, OPT_SAFE_SCALING, OPT_STAT_COPIES, TOPOLOGY, TOPOLOGY_NAME, IterRecord, Status, check, lib
 
 IterCallback = Callable[[int, float, float], None]
 
@@ -104,7 +104,8 @@ class BaumWelchEngine:
     """Baum-Welch training / scoring of one discrete HMM (N states, M symbols) on one GPU."""
 
     def __init__(self, n_states: int, n_symbols: int, device: Optional[int] = None, topology: str = "auto",
-                 rank: int = 0, world_size: int = 1, stream: Optional[int] = None, safe_scaling: bool = False):
+                 rank: int = 0, world_size: int = 1, stream: Optional[int] = None, safe_scaling: bool = False,
+                 fuse_mstep: bool = False, stat_copies: int = 1):
         self._lib = lib()
         self.N, self.M = int(n_states), int(n_symbols)
         self.device = default_device() if device is None else int(device)
@@ -121,6 +122,10 @@ class BaumWelchEngine:
         check(self._lib.hmmbw_set_topology(self._ctx, TOPOLOGY[topology]))
         if safe_scaling:
             check(self._lib.hmmbw_set_option(self._ctx, OPT_SAFE_SCALING, 1))
+        if fuse_mstep:
+            check(self._lib.hmmbw_set_option(self._ctx, OPT_FUSE_MSTEP, 1))
+        if stat_copies != 1:
+            check(self._lib.hmmbw_set_option(self._ctx, OPT_STAT_COPIES, int(stat_copies)))
         self.n_seq = 0
         self.n_seq_global = 0
 

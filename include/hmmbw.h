@@ -134,9 +134,15 @@ int hmmbw_score(hmmbw_ctx *ctx, double *out);
 /* Number of statistics accumulator copies the E-step's workgroups spread their atomics over
  * (workgroup b adds into copy b % n; default 1). */
 #define HMMBW_OPT_STAT_COPIES 3
+/* 1: hmmbw_iterate runs the M-step in the last E-step workgroup to finish instead of a second
+ * kernel (cross-workgroup data through memory-side atomics).  Default 0. */
+#define HMMBW_OPT_FUSE_MSTEP 4
 int hmmbw_set_option(hmmbw_ctx *ctx, int key, int64_t value);
 
-/* E-step kernel timing with HIP events on the context stream (for bench/roofline). */
+/* E-step kernel timing with HIP events on the context stream (for bench/roofline).  Returns the
+ * accumulated time and count of the timed launches so far, then (enable >= 0) resets and sets the
+ * mode: 0 off, k >= 1 record events around every k-th E-step launch (sampling keeps the event
+ * overhead out of the timed loop); enable < 0 only queries. */
 int hmmbw_timing(hmmbw_ctx *ctx, int enable, double *total_ms, int64_t *count);
 
 #ifdef __cplusplus

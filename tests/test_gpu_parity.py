@@ -303,3 +303,23 @@ def test_pathological_emissions_fall_back_to_safe_scaling(topology, equal_length
     assert_params(A2, ref.A, "A")
     assert_params(B2, ref.B, "B")
     assert_params(p2, ref.pi, "pi")
+
+
+@pytest.mark.parametrize("fuse,copies", [(True, 1), (True, 4), (False, 4)])
+@pytest.mark.parametrize("case", ["n8_k256_cfg2", "n4_k16_default", "converge", "dense_n6"])
+def test_engine_variants_match_reference(case, fuse, copies):
+    """The fused-M-step and multi-copy accumulation variants give the reference's results."""
+    from hmm_training_amd.engine import BaumWelchEngine
+    d = load(case)
+    N, M = int(d["N"]), int(d["M"])
+    with BaumWelchEngine(N, M, fuse_mstep=fuse, stat_copies=copies) as eng:
+        eng.set_observations(observations(d))
+        eng.set_params(d["init_pi"], d["init_A"], d["init_B"])
+        trace = []
+        st = eng.train(float(d["epsilon"]), int(d["max_iterations"]), lambda k, L, df: trace.append(L))
+        assert st.iterations == int(d["iterations"])
+        assert_ll(trace, d["trace_L"])
+        pi, A, B = eng.params(normalise=True)
+    assert_params(A, d["out_A"], "A")
+    assert_params(B, d["out_B"], "B")
+    assert_params(pi, d["out_pi"], "pi")
