@@ -51,6 +51,7 @@ def parse():
     p.add_argument("--seed", type=int, default=3)
     p.add_argument("--no-kernel-timing", action="store_true", help="skip the HIP events")
     p.add_argument("--timing-every", type=int, default=5, help="time every k-th E-step launch")
+    p.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) on MI355X; gloo only for tests")
     return p.parse_args()
 
 
@@ -110,10 +111,13 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    device = local_rank % max(torch.cuda.device_count(), 1) if world > 1 else 0
     if world > 1:
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    device = local_rank if world > 1 else 0
+        torch.cuda.set_device(device)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+        else:
+            dist.init_process_group(args.dist_backend)
     torch.cuda.set_device(device)
 
     from hmm_training_amd.engine import BaumWelchEngine

@@ -323,3 +323,93 @@ def test_engine_variants_match_reference(case, fuse, copies):
     assert_params(A, d["out_A"], "A")
     assert_params(B, d["out_B"], "B")
     assert_params(pi, d["out_pi"], "pi")
+
+
+@pytest.mark.parametrize("case", ["n8_k256_t200", "converge", "zero_prob_seq", "dense_n16", "n64_k1024_tiny"])
+@pytest.mark.parametrize("world", [2, 3])
+def test_multirank_estep_mstep_in_process(case, world):
+    """The multi-rank path (hmmbw_estep -> sum of the packed statistics -> hmmbw_mstep) with `world`
+    engines in one process on cuda:0; the all-reduce is a torch sum.  Must match the reference run
+    on the unsharded data (hmm_training.py:351-514)."""
+    import torch
+    from hmm_training_amd.engine import BaumWelchEngine, shard_bounds
+    d = load(case)
+    N, M = int(d["N"]), int(d["M"])
+    obs = observations(d)
+    bounds = shard_bounds([len(o) for o in obs], world)
+    if any(hi <= lo for lo, hi in bounds):
+        pytest.skip("a rank would be empty")
+    engines, bufs = [], []
+    for r, (lo, hi) in enumerate(bounds):
+        e = BaumWelchEngine(N, M, rank=r, world_size=world)
+        e.set_observations(obs[lo:hi], n_seq_global=len(obs))
+        engines.append(e)
+    for e in engines:
+        e.set_params(d["init_pi"], d["init_A"], d["init_B"])
+        e.reset(float(d["epsilon"]), int(d["max_iterations"]))
+        bufs.append(e.make_stats_buffer())
+    import ctypes
+    from hmm_training_amd._lib import check
+    for _ in range(int(d["max_iterations"]) + 1):
+        for e, b in zip(engines, bufs):
+            check(e._lib.hmmbw_estep(e._ctx, ctypes.c_void_p(b.data_ptr())))
+        tot = torch.stack(bufs).sum(0)
+        for e, b in zip(engines, bufs):
+            b.copy_(tot)
+            check(e._lib.hmmbw_mstep(e._ctx, ctypes.c_void_p(b.data_ptr()), len(obs)))
+    torch.cuda.synchronize()
+    for e in engines:
+        st, recs = e.status(0, int(d["iterations"]))
+        assert st.done and st.iterations == int(d["iterations"])
+        assert_ll([L for L, _ in recs], d["trace_L"])
+        pi, A, B = e.params(normalise=True)
+        assert_params(A, d["out_A"], "A")
+        assert_params(B, d["out_B"], "B")
+        assert_params(pi, d["out_pi"], "pi")
+        e.close()
+
+
+def _dropin_worker(rank, world, port, case, tmp, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from hmm_training_amd.hmm_training import hmm_training
+        d = load(case)
+        buf = io.StringIO()
+        with contextlib.redirect_stdout(buf):
+            A, B, pi = hmm_training(observations(d), N=int(d["N"]), M=int(d["M"]), epsilon=float(d["epsilon"]),
+                                    max_iterations=int(d["max_iterations"]), show_progress=True,
+                                    load_initial_params=False)
+        q.put((rank, A, B, pi, buf.getvalue().splitlines()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("case", ["n4_k256_default", "n4_k16_default"])
+def test_dropin_two_processes_gloo(case, tmp_path):
+    """hmm_training under an initialised process group (2 ranks on the one GPU, gloo carrying the
+    all-reduce of the device statistics buffer): every rank returns the reference's (A, B, pi)."""
+    import multiprocessing as mp
+    import socket
+    d = load(case)
+    if bool(d["load_initial"]):
+        pytest.skip("warm-start case")
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_dropin_worker, args=(r, 2, port, case, str(tmp_path), q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, A, B, pi, lines in res:
+        assert_params(A, d["out_A"], f"A rank {rank}")
+        assert_params(B, d["out_B"], f"B rank {rank}")
+        assert_params(pi, d["out_pi"], f"pi rank {rank}")
+        if rank == 0:
+            assert lines == list(d["stdout"])
