@@ -38,7 +38,7 @@ EXPORTED = (
 OPT_SAFE_SCALING = 1
 OPT_ABLATE = 2
 OPT_STAT_COPIES = 3
-OPT_FUSE_MSTEP = 4
+OPT_MERGE_MSTEP = 4
 
 
 class HMMBWError(RuntimeError):

@@ -19,13 +19,15 @@
 //   k_estep_small<N,G,LR,LDSTAB,FWD_ONLY>  N <= 16: a sequence is a group of G = pow2ceil(N) lanes,
 //        lane j = state j, 64/G sequences per wavefront.  Cross-lane exchange by DPP (quad_perm,
 //        row_shr/shl, row_half_mirror, row_mirror, row_newbcast); B^T and the B-numerator histogram
-//        in LDS; alpha_hat spilled to HBM coalesced (512 B per wave-step) and re-read by the
-//        backward sweep, which fuses beta, gamma, xi and the histogram scatter.
+//        in LDS; the forward sweep stores one alpha_hat checkpoint per 8-step chunk plus the int16
+//        scale exponents, the backward sweep recomputes each chunk's alpha_hat in registers
+//        (bit-identical) and fuses beta, gamma, xi and the histogram scatter.
 //   k_estep_wide<NP,FWD_ONLY>              16 < N <= 64: one sequence per wavefront, lane = state,
 //        A / A^T in LDS, alpha / v exchanged through a per-wave LDS row.
 //   k_reduce_local  (multi-rank) sum the statistics copies into the all-reduce buffer + the rank's
 //                   (max, sum exp) pair of log P_r.
-//   k_mstep     one workgroup: L, M-step, convergence record, zero the statistics.
+//   k_mstep / k_mstep_staged  one workgroup: L, M-step, convergence record, zero the statistics
+//                   (staged: all statistics gathered into LDS with one batch of loads).
 //   k_finalise  the reference's return-path normalisation (:524-541).
 #include <hip/hip_runtime.h>
 
@@ -42,6 +44,22 @@
 #include "../../include/hmmbw.h"
 
 namespace hmmbw {
+
+// Diagnostics build only (-DHMMBW_PHASE_TIMES, tools/phase_times.py): per-wave wall-clock stamps of
+// the small E-step's phases, read back with hmmbw_debug_phase_times.
+#ifdef HMMBW_PHASE_TIMES
+constexpr int kPhaseWaves = 1 << 16;
+__device__ unsigned long long g_phase[kPhaseWaves][8];
+#define PHASE(k)                                                                               \
+    do {                                                                                       \
+        const long long w_ = (long long)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);   \
+        if ((threadIdx.x & 63) == 0 && w_ < kPhaseWaves) g_phase[w_][k] = wall_clock64();      \
+    } while (0)
+#else
+#define PHASE(k) \
+    do {         \
+    } while (0)
+#endif
 
 constexpr int kWave = 64;
 constexpr int kChunk = 8;  // time steps per packed symbol load (8 x uint16 = 16 B)
@@ -87,7 +105,8 @@ struct MArgs {
     const double *llpart;
     long long nblocks;
     long long R_global;
-    IterState *state;
+    const IterState *state;  // convergence state entering this M-step
+    IterState *state_out;    // ... and after it (double-buffered: the host flips the slots per M-step)
     double *hist;
     int N, K, G, world;
     int local_lse;
@@ -112,8 +131,9 @@ struct EArgs {
     int N;
     int force_safe;    // 1: per-step normalisation (no lagged scaling)
     int ablate;        // diagnostics only: bit 0 skips the statistics flush, bit 1 the backward sweep
-    int fused;         // 1: the last workgroup to finish runs the M-step (single rank)
-    unsigned *ticket;  // workgroup completion counter for the fused M-step
+    int merged;        // 1: run the previous iteration's M-step (m) in the prologue of every workgroup
+    double *zero;      // statistics buffer of the NEXT iteration, cleared by this launch (or nullptr)
+    long long zero_len;
     MArgs m;
     long long off_S, off_gex, off_gall, off_bnum;
 };
@@ -236,11 +256,11 @@ __device__ void block_ll_partial(double lp, bool valid, double *sh, double *out)
 // ---------------------------------------------------------------------------------------------
 // Small-N E-step / scorer.  One G-lane group per sequence (lane j = state j), 64/G per wave.
 //
-// Forward: z_t = alpha_t / 2^{C_t}, C_t = s_0 + ... + s_t.  In the default (lagged) mode the scale
-// exponent applied at step t is chosen two steps early, s_t = M_{t-2} - s_{t-1} with M = the group's
-// largest frexp exponent, so that C_t tracks log2 of alpha_{t-2}'s magnitude and the per-step
-// dependency chain is just (DPP shift || multiply) -> fma; the scaling itself is folded into the
-// emission factor b_j(o_t) * 2^{-s_t} (exact).  If a wave's magnitudes ever leave [2^-900, 2^900]
+// Forward: z_t = alpha_t / 2^{C_t}, C_t = s_0 + ... + s_t.  In the default (lagged) mode only every
+// kScale-th step rescales, by s_t = M_{t-kScale} - 1023 with M = the biased exponent of the group's
+// largest entry measured kScale steps earlier, so the per-step dependency chain is just
+// (DPP shift || multiply) -> fma; the scaling itself is folded into the emission factor
+// b_j(o_t) * 2^{-s_t} (exact).  If a wave's magnitudes ever leave [2^-900, 2^900]
 // (pathological parameters) the wave re-runs its forward in the safe mode, which normalises every
 // step by its own group maximum.  Only z at the first step of every 8-step chunk (the checkpoint)
 // and the s_t are stored; the backward sweep recomputes each chunk's z_t in registers with the
@@ -251,7 +271,8 @@ __device__ void block_ll_partial(double lp, bool valid, double *sh, double *out)
 //   gamma_t(i) = z_t(i) beta_hat_t(i),  xi_t(i,j) = a_ij z_t(i) v_j  (accumulated as S_ij = xi/a_ij).
 // gamma is scattered into the per-workgroup LDS histogram B_num[o_t][j] (ds_add_f64).
 // ---------------------------------------------------------------------------------------------
-__device__ void estep_tail(const EArgs &a, double *lds);
+template <int N, int G, int GP, bool HIST>
+__device__ bool merged_mstep(const EArgs &a, double *sBt, double *sBn, double *sPA);
 
 template <int N, int G, bool LR, bool LDSTAB, bool FWD_ONLY>
 __global__ void __launch_bounds__(kBlock) k_estep_small(EArgs a) {
@@ -260,24 +281,58 @@ __global__ void __launch_bounds__(kBlock) k_estep_small(EArgs a) {
     constexpr int NV = NS + 3;          // + gamma_den_excl, gamma_den_all, pi_num
     constexpr int GP = LDSTAB ? G + 1 : G;  // row stride of the emission / histogram tables
     extern __shared__ double smem[];
-    if (a.state != nullptr && a.state->done) return;  // converged: device-side no-op
-
+    __shared__ double sPA[G + N * N];  // pi (zero-padded to G) and A of this iteration
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    PHASE(0);
+    if constexpr (!FWD_ONLY)  // clear the next iteration's statistics (single rank: triple buffer)
+        for (long long i = (long long)blockIdx.x * blockDim.x + tid; i < a.zero_len;
+             i += (long long)gridDim.x * blockDim.x)
+            a.zero[i] = 0.0;
     const int j = lane & (G - 1), u = lane / G;
     const int K = a.K;
     double *sBt = smem;                                               // [K][GP] + pad
     double *sBn = smem + (LDSTAB ? (size_t)K * GP + GP : 0);          // [K][GP]
     double *sRed = sBn + ((LDSTAB && !FWD_ONLY) ? (size_t)K * GP : 0); // [waves][G][NV] + ll scratch
-    if constexpr (LDSTAB) {
-        for (int i = tid; i < (K + 1) * GP; i += blockDim.x) {
-            const int k = i / GP, c = i - k * GP;
-            sBt[i] = (k < K && c < G) ? a.Bt[(size_t)k * G + c] : 0.0;
-            if constexpr (!FWD_ONLY)
-                if (k < K) sBn[i] = 0.0;
+    bool merged = false;
+    if constexpr (LDSTAB && !FWD_ONLY) merged = a.merged != 0;
+    if (merged) {
+        // the previous iteration's M-step, computed redundantly by every workgroup straight into
+        // its LDS tables (no separate M-step kernel, no parameter round trip through HBM)
+        if constexpr (LDSTAB && !FWD_ONLY)
+            if (!merged_mstep<N, G, GP, true>(a, sBt, sBn, sPA)) return;  // done or stopped (:346)
+    } else {
+        if (a.state != nullptr && a.state->done) return;  // converged: device-side no-op
+        if (tid < G) sPA[tid] = tid < N ? a.pi[tid] : 0.0;
+        if (tid < N * N) sPA[G + tid] = a.A[tid];
+        if constexpr (LDSTAB) {
+            // 16 independent loads in flight per thread before the first LDS store
+            constexpr int TB = 16;
+            const int nt = (K + 1) * GP;
+            for (int i0 = 0; i0 < nt; i0 += TB * kBlock) {
+                double x[TB];
+#pragma unroll
+                for (int q = 0; q < TB; ++q) {
+                    const int i = i0 + q * kBlock + tid;
+                    const int k = i / GP, c = i - k * GP;
+                    const bool ok = i < nt && k < K && c < G;
+                    x[q] = a.Bt[ok ? (size_t)k * G + c : 0];
+                    x[q] = ok ? x[q] : 0.0;
+                }
+#pragma unroll
+                for (int q = 0; q < TB; ++q) {
+                    const int i = i0 + q * kBlock + tid;
+                    if (i < nt) {
+                        sBt[i] = x[q];
+                        if constexpr (!FWD_ONLY)
+                            if (i < K * GP) sBn[i] = 0.0;
+                    }
+                }
+            }
         }
+        __syncthreads();
     }
-    __syncthreads();
     const double *Btab = LDSTAB ? sBt : a.Bt;
+    PHASE(1);
 
     const long long wave = (long long)blockIdx.x * (blockDim.x >> 6) + wv;
     double *accb = a.copies + (long long)(blockIdx.x % a.ncopies) * a.copy_len;
@@ -303,18 +358,19 @@ __global__ void __launch_bounds__(kBlock) k_estep_small(EArgs a) {
         // transition coefficients of this lane (state j)
         double acol[LR ? 1 : N], arow[LR ? 1 : N];
         double a_dg = 0.0, a_in = 0.0, a_up = 0.0;
+        const double *sA = sPA + G;
         if constexpr (LR) {
-            a_dg = jv ? a.A[j * N + j] : 0.0;
-            a_in = (jv && j >= 1) ? a.A[(j - 1) * N + j] : 0.0;
-            a_up = (j + 1 < N) ? a.A[j * N + j + 1] : 0.0;
+            a_dg = jv ? sA[j * N + j] : 0.0;
+            a_in = (jv && j >= 1) ? sA[(j - 1) * N + j] : 0.0;
+            a_up = (j + 1 < N) ? sA[j * N + j + 1] : 0.0;
         } else {
 #pragma unroll
             for (int i = 0; i < N; ++i) {
-                acol[i] = jv ? a.A[i * N + j] : 0.0;
-                arow[i] = jv ? a.A[j * N + i] : 0.0;
+                acol[i] = jv ? sA[i * N + j] : 0.0;
+                arow[i] = jv ? sA[j * N + i] : 0.0;
             }
         }
-        const double pij = jv ? a.pi[j] : 0.0;
+        const double pij = sPA[j];
 
         auto loadpack = [&](int c) -> uint4 {
             return *reinterpret_cast<const uint4 *>(symw + (long long)c * U * kChunk);
@@ -434,6 +490,7 @@ __global__ void __launch_bounds__(kBlock) k_estep_small(EArgs a) {
             else forward(std::true_type{}, std::true_type{});
         }
 
+        PHASE(2);
         // log P(O|lambda) = log(sum_j z_{T-1}(j)) + ln2 * C   (:375-377)
         const double phat = gsum<G>(z);
         const bool alive = (T > 0) && (phat > 0.0);
@@ -504,7 +561,7 @@ __global__ void __launch_bounds__(kBlock) k_estep_small(EArgs a) {
                             const double vd = f * beta, vu = fu * bup;
                             bn = fma(a_up, vu, a_dg * vd);       // :182-197
                             S[0] = fma(zs, vd, S[0]);             // xi_t(j,j)   / a_jj
-                            S[1] = fma(zs, vu, S[1]);             // xi_t(j,j+1) / a_j,j+1
+                            S[1] = fma(zs, vu, S[1]);             // xi_t(j,j+1) / a_j,j+1 (scaled at the end)
                         } else {
                             const double vd = f * beta;
                             double b0 = 0.0, b1 = 0.0;
@@ -564,12 +621,20 @@ __global__ void __launch_bounds__(kBlock) k_estep_small(EArgs a) {
                 else backward(std::false_type{}, std::true_type{});
             }
             gall += gex;
+            PHASE(3);
+            // xi_t(i,j) = a_ij * (the accumulated S_ij): scale once per sequence group
+#pragma unroll
+            for (int k = 0; k < NS; ++k) {
+                if constexpr (LR) S[k] *= (k == 0 ? a_dg : a_up);
+                else S[k] *= arow[k];
+            }
         }
     }
 
     // per-block (max, sum exp) of log P for the convergence scalar
     __syncthreads();
     block_ll_partial(logp_lane, ll_valid, sRed, a.llpart + 2 * (long long)blockIdx.x);
+    PHASE(4);
 
     if constexpr (!FWD_ONLY) if (!(a.ablate & 1)) {
         // ---- reduce per-lane accumulators over the U sequences of the wave, then the block ----
@@ -621,8 +686,7 @@ __global__ void __launch_bounds__(kBlock) k_estep_small(EArgs a) {
             }
         }
     }
-    if constexpr (!FWD_ONLY)
-        if (a.fused) estep_tail(a, smem);
+    PHASE(5);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -750,7 +814,8 @@ __global__ void __launch_bounds__(kBlock) k_estep_wide(EArgs a) {
         if (jv) {
 #pragma unroll
             for (int k = 0; k < NP; ++k)
-                if (k < N && S[k] != 0.0) unsafeAtomicAdd(&accb[a.off_S + (long long)j * N + k], S[k]);
+                if (k < N && S[k] != 0.0)  // xi_t(j,k) = a_jk * S_jk
+                    unsafeAtomicAdd(&accb[a.off_S + (long long)j * N + k], S[k] * sAT[k * 64 + j]);
             if (gex != 0.0) unsafeAtomicAdd(&accb[a.off_gex + j], gex);
             if (gall != 0.0) unsafeAtomicAdd(&accb[a.off_gall + j], gall);
             if (pin != 0.0) unsafeAtomicAdd(&accb[j], pin);
@@ -860,13 +925,49 @@ __device__ __forceinline__ double take(const MArgs &m, long long idx) {
     return v;
 }
 
+// B entry from its numerator and the reciprocal of its row's denominator (:460-497): 1e-20 floor when
+// no gamma term carries the symbol, 0 for an empty row.  Shared by every M-step variant, so they
+// produce bit-identical parameters.
+__device__ __forceinline__ double mstep_inv(double den) { return den > 0.0 ? 1.0 / den : 0.0; }
+__device__ __forceinline__ double bnum_to_b(double num, double inv) {
+    return inv > 0.0 ? (num > 0.0 ? num * inv : 1e-20) : 0.0;
+}
+
+// Convergence record of one EM iteration (hmm_training.py:503-514): L of the parameters that entered
+// it, diff (+inf on the first iteration), the stop rule of :346; written to the next state slot.
+__device__ bool record_iteration(const MArgs &m, const IterState &in, double L) {
+    const double diff = (in.prev_L != -INFINITY) ? fabs(L - in.prev_L) : INFINITY;  // :505-508
+    const long long it = in.iteration;
+    const bool cont = (diff >= in.epsilon) && (it + 1 < in.max_iterations);
+    m.hist[2 * (it % kHist)] = L;
+    m.hist[2 * (it % kHist) + 1] = diff;
+    IterState o = in;
+    o.prev_L = L;
+    o.last_L = L;
+    o.last_diff = diff;
+    o.iteration = it + 1;
+    if (!cont) {
+        o.done = 1;
+        o.converged = (it + 1 < in.max_iterations) ? 1 : 0;
+    }
+    *m.state_out = o;
+    return cont;
+}
+
+// M-step kernels entered after convergence carry the state over to the next slot and do nothing else
+__device__ __forceinline__ bool carry_if_done(const MArgs &m) {
+    if (!m.state->done) return false;
+    if (threadIdx.x == 0 && blockIdx.x == 0) *m.state_out = *m.state;
+    return true;
+}
+
 // M-step + convergence by one workgroup of 256 threads (hmm_training.py:415-514).
 template <bool ATOMIC>
 __device__ void mstep_block(const MArgs &m) {
     __shared__ double sh[16];
     __shared__ double sL;
     __shared__ double sPi[64], sGex[64], sGall[64];
-    IterState *st = m.state;
+    const IterState *st = m.state;
     const int tid = threadIdx.x;
     // L = LSE_r log P_r over all ranks (:503)
     if (m.local_lse) {
@@ -894,43 +995,26 @@ __device__ void mstep_block(const MArgs &m) {
     __syncthreads();
     // pi (:415-424): LSE_r gamma_0 - log R ; no term -> -inf
     for (int i = tid; i < N; i += blockDim.x) m.pi[i] = sPi[i] > 0.0 ? sPi[i] / (double)m.R_global : 0.0;
-    // A (:429-455): xi numerator = a_ij * S_ij ; denominator excludes the last frame
+    // A (:429-455): xi numerator; denominator excludes the last frame
     for (int idx = tid; idx < N * N; idx += blockDim.x) {
         const double den = sGex[idx / N];
-        const double num = m.A[idx] * take<ATOMIC>(m, m.off_S + idx);
+        const double num = take<ATOMIC>(m, m.off_S + idx);
         m.A[idx] = (den > 0.0 && num > 0.0) ? num / den : 0.0;
     }
     // B (:460-497): floor 1e-20 when no gamma term carries the symbol; empty denominator -> row 0
     for (long long idx = tid; idx < (long long)N * K; idx += blockDim.x) {
         const int jj = (int)(idx % N), k = (int)(idx / N);  // symbol-major: coalesced over the copies
-        const double den = sGall[jj];
         const double num = take<ATOMIC>(m, m.off_bnum + idx);
-        const double v = den > 0.0 ? (num > 0.0 ? num / den : 1e-20) : 0.0;
+        const double v = bnum_to_b(num, mstep_inv(sGall[jj]));
         m.B[(long long)jj * K + k] = v;
         m.Bt[(long long)k * m.G + jj] = v;
     }
     __syncthreads();
-    if (tid == 0) {
-        const double L = sL;
-        const double prev = st->prev_L;
-        const double diff = (prev != -INFINITY) ? fabs(L - prev) : INFINITY;  // :505-508
-        const long long it = st->iteration;
-        m.hist[2 * (it % kHist)] = L;
-        m.hist[2 * (it % kHist) + 1] = diff;
-        st->prev_L = L;
-        st->last_L = L;
-        st->last_diff = diff;
-        st->iteration = it + 1;
-        const bool cont = (diff >= st->epsilon) && (it + 1 < st->max_iterations);  // :346
-        if (!cont) {
-            st->done = 1;
-            st->converged = (it + 1 < st->max_iterations) ? 1 : 0;
-        }
-    }
+    if (tid == 0) record_iteration(m, *st, sL);
 }
 
 __global__ void __launch_bounds__(256) k_mstep(MArgs m) {
-    if (m.state->done) return;
+    if (carry_if_done(m)) return;
     mstep_block<false>(m);
 }
 
@@ -954,22 +1038,15 @@ __device__ void mstep_staged(const MArgs &m, double *sSt) {
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, nw = blockDim.x >> 6;
     const int N = m.N, K = m.K;
     const long long len = m.copy_len;
-    // ---- one batch of independent loads: old A, convergence state, LL pairs, statistics ----
-    const double a_old = tid < N * N ? m.A[tid] : 0.0;  // N*N <= 256 for the staged path
-    double prev = 0.0, eps = 0.0;
-    long long it = 0, maxit = 0;
-    if (tid == 0) {
-        prev = m.state->prev_L;
-        eps = m.state->epsilon;
-        it = m.state->iteration;
-        maxit = m.state->max_iterations;
-    }
+    // ---- one batch of independent loads: convergence state, LL pairs, statistics ----
+    IterState in{};
+    if (tid == 0) in = *m.state;
     // Branch-free, clamped addresses so the compiler issues every load of a batch before the first
     // wait (a guarded load inside a runtime loop serialises on its own s_waitcnt).
     constexpr int PB = 4;
     double pm[PB], ps[PB];
     double M = -INFINITY, S = 0.0;
-    const long long nb = m.nblocks;
+    const long long nb = m.nblocks;  // >= 1 (a launch with no workgroups leaves nothing pending)
     for (long long r0 = 0; r0 < nb; r0 += (long long)PB * blockDim.x) {
 #pragma unroll
         for (int u = 0; u < PB; ++u) {
@@ -1028,61 +1105,191 @@ __device__ void mstep_staged(const MArgs &m, double *sSt) {
     if (tid < N) m.pi[tid] = sPi[tid] > 0.0 ? sPi[tid] / (double)m.R_global : 0.0;
     if (tid < N * N) {
         const double den = sGex[tid / N];
-        const double num = a_old * sS_[tid];
+        const double num = sS_[tid];
         m.A[tid] = (den > 0.0 && num > 0.0) ? num / den : 0.0;
     }
     for (int idx = tid; idx < N * K; idx += blockDim.x) {
         const int k = idx / N, jj = idx - k * N;
-        const double den = sGall[jj];
-        const double num = sBn[idx];
-        const double v = den > 0.0 ? (num > 0.0 ? num / den : 1e-20) : 0.0;
+        const double v = bnum_to_b(sBn[idx], mstep_inv(sGall[jj]));
         m.B[(long long)jj * K + k] = v;
         m.Bt[(long long)k * m.G + jj] = v;
     }
+    if (tid == 0) record_iteration(m, in, sL);
+}
+
+// The previous iteration's M-step + convergence step (hmm_training.py:415-514), run by EVERY
+// workgroup of the merged E-step launch, straight into its LDS tables: every workgroup reads the same
+// statistics and log-likelihood pairs and applies the same arithmetic in the same order, so all of
+// them hold bit-identical parameters and reach the same stop decision.  Workgroup 0 also writes the
+// parameters back to HBM (for the queries) and records the iteration in the other state slot.
+// Returns false when EM stops here (or had stopped before).
+constexpr int kMergedMaxStats = 16 * kBlock;  // statistics per launch the prologue holds in registers
+
+__device__ __forceinline__ double wave_max(double x) {
+    x = fmax(x, dpp<0xB1>(x));
+    x = fmax(x, dpp<0x4E>(x));
+    x = fmax(x, dpp<0x141>(x));
+    x = fmax(x, dpp<0x140>(x));
+    x = fmax(x, __shfl_xor(x, 16));
+    return fmax(x, __shfl_xor(x, 32));
+}
+
+template <int N, int G, int GP, bool HIST>
+__device__ bool merged_mstep(const EArgs &a, double *sBt, double *sBn, double *sPA) {
+    constexpr int NSM = N + N * N + 2 * N;  // pi_num, xi, gamma_den_excl, gamma_den_all
+    constexpr int NW = kBlock / 64;
+    constexpr int SB = kMergedMaxStats / kBlock;
+    constexpr int PB = 2;                   // log-likelihood pairs per thread per pass
+    __shared__ double sSm[NSM];
+    __shared__ double sMx[NW], sSum[NW];
+    __shared__ IterState sIn;
+    const MArgs &m = a.m;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int K = a.K;
+    const long long len = m.copy_len;
+    // ---- every load issued before any use: statistics, log-likelihood pairs, convergence state ----
+    double v[SB];
+#pragma unroll
+    for (int q = 0; q < SB; ++q) {
+        const long long idx = (long long)q * kBlock + tid;
+        v[q] = m.src[idx < len ? idx : len - 1];
+    }
+    for (int c = 1; c < m.nsrc; ++c) {
+        double x[SB];
+#pragma unroll
+        for (int q = 0; q < SB; ++q) {
+            const long long idx = (long long)q * kBlock + tid;
+            x[q] = m.src[c * len + (idx < len ? idx : len - 1)];
+        }
+#pragma unroll
+        for (int q = 0; q < SB; ++q) v[q] += x[q];
+    }
+    const long long nb = m.nblocks;  // >= 1
+    double pm[PB], ps[PB];
+#pragma unroll
+    for (int q = 0; q < PB; ++q) {
+        const long long r = (long long)q * kBlock + tid;
+        const long long rc = r < nb ? r : nb - 1;
+        pm[q] = m.llpart[2 * rc];
+        ps[q] = m.llpart[2 * rc + 1];
+    }
+    IterState in{};
     if (tid == 0) {
-        IterState *st = m.state;
-        const double L = sL;
-        const double diff = (prev != -INFINITY) ? fabs(L - prev) : INFINITY;  // :505-508
-        m.hist[2 * (it % kHist)] = L;
-        m.hist[2 * (it % kHist) + 1] = diff;
-        st->prev_L = L;
-        st->last_L = L;
-        st->last_diff = diff;
-        st->iteration = it + 1;
-        const bool cont = (diff >= eps) && (it + 1 < maxit);  // :346
-        if (!cont) {
-            st->done = 1;
-            st->converged = (it + 1 < maxit) ? 1 : 0;
+        in.prev_L = m.state->prev_L;
+        in.epsilon = m.state->epsilon;
+        in.iteration = m.state->iteration;
+        in.max_iterations = m.state->max_iterations;
+        in.done = m.state->done;
+        in.converged = m.state->converged;
+        in.last_L = m.state->last_L;
+        in.last_diff = m.state->last_diff;
+    }
+    // ---- L = LSE_r log P_r (:503) in two passes: max, then sum of exp(m - max) ----
+    double mx = -INFINITY;
+#pragma unroll
+    for (int q = 0; q < PB; ++q) {
+        const bool ok = (long long)q * kBlock + tid < nb && ps[q] > 0.0;
+        mx = ok ? fmax(mx, pm[q]) : mx;
+    }
+    for (long long r = (long long)PB * kBlock + tid; r < nb; r += kBlock)  // > 512 workgroups
+        if (m.llpart[2 * r + 1] > 0.0) mx = fmax(mx, m.llpart[2 * r]);
+    mx = wave_max(mx);
+    if (lane == 0) sMx[wv] = mx;
+#pragma unroll
+    for (int q = 0; q < SB; ++q) {
+        const int idx = q * kBlock + tid;
+        if (idx < NSM) sSm[idx] = (idx < len) ? v[q] : 0.0;
+    }
+    if (tid == 0) sIn = in;
+    __syncthreads();
+    PHASE(6);
+    if (sIn.done) {  // converged before this launch: device-side no-op
+        if (tid == 0 && blockIdx.x == 0) *m.state_out = sIn;
+        return false;
+    }
+    double Mb = sMx[0];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) Mb = fmax(Mb, sMx[w]);
+    double sum = 0.0;
+    if (Mb != -INFINITY) {
+#pragma unroll
+        for (int q = 0; q < PB; ++q) {
+            const bool ok = (long long)q * kBlock + tid < nb && ps[q] > 0.0;
+            sum += ok ? ps[q] * exp(pm[q] - Mb) : 0.0;
+        }
+        for (long long r = (long long)PB * kBlock + tid; r < nb; r += kBlock)
+            if (m.llpart[2 * r + 1] > 0.0) sum += m.llpart[2 * r + 1] * exp(m.llpart[2 * r] - Mb);
+    }
+    sum = gsum<64>(sum);
+    if (lane == 0) sSum[wv] = sum;
+    PHASE(7);
+    // pi (:415-424), A (:429-455) into LDS
+    if (tid < G) sPA[tid] = (tid < N && sSm[tid] > 0.0) ? sSm[tid] / (double)m.R_global : 0.0;
+    if (tid < N * N) {
+        const double den = sSm[N + N * N + tid / N];
+        const double num = sSm[N + tid];
+        sPA[G + tid] = (den > 0.0 && num > 0.0) ? num / den : 0.0;
+    }
+    // B (:460-497) from the registers straight into the emission table (and HBM, workgroup 0).
+    // Element e = q * kBlock + tid - NSM is symbol e / N, state e % N; with N | kBlock the state (and
+    // so the denominator) is the same for every q of a thread: one reciprocal per thread.
+    const bool w0 = blockIdx.x == 0;
+    const int e0 = tid - NSM;
+    constexpr bool kSameState = (kBlock % N) == 0;
+    const int jj0 = ((e0 % N) + N) % N;
+    const double inv0 = kSameState ? mstep_inv(sSm[N + N * N + N + jj0]) : 0.0;
+    double bval[SB];
+#pragma unroll
+    for (int q = 0; q < SB; ++q) {
+        const int e = q * kBlock + e0;
+        const int jj = kSameState ? jj0 : ((e % N) + N) % N;
+        const double inv = kSameState ? inv0 : mstep_inv(sSm[N + N * N + N + jj]);
+        bval[q] = bnum_to_b(v[q], inv);
+        if (e >= 0 && e < K * N) sBt[(e / N) * GP + jj] = bval[q];
+    }
+    if (w0) {
+#pragma unroll
+        for (int q = 0; q < SB; ++q) {
+            const int e = q * kBlock + e0;
+            if (e >= 0 && e < K * N) {
+                const int k = e / N, jj = e - k * N;
+                m.B[(long long)jj * K + k] = bval[q];
+                m.Bt[(long long)k * G + jj] = bval[q];
+            }
         }
     }
+    // zero the pad columns [N, GP) of every row and the pad row K; clear the histogram
+    for (int i = tid; i < (K + 1) * (GP - N); i += kBlock) {
+        const int k = i / (GP - N), c = N + (i - k * (GP - N));
+        sBt[k * GP + c] = 0.0;
+    }
+    if (tid < N) sBt[K * GP + tid] = 0.0;
+    if constexpr (HIST) {
+        double2 *z2 = reinterpret_cast<double2 *>(sBn);
+        for (int i = tid; i < K * GP / 2; i += kBlock) z2[i] = double2{0.0, 0.0};
+        if ((K * GP) & 1)
+            if (tid == 0) sBn[K * GP - 1] = 0.0;
+    }
+    __syncthreads();
+    double S = 0.0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) S += sSum[w];
+    const double L = (S > 0.0) ? Mb + log(S) : -INFINITY;
+    const double diff = (sIn.prev_L != -INFINITY) ? fabs(L - sIn.prev_L) : INFINITY;  // :505-508
+    const bool cont = (diff >= sIn.epsilon) && (sIn.iteration + 1 < sIn.max_iterations);  // :346
+    if (w0) {
+        if (tid < N) m.pi[tid] = sPA[tid];
+        if (tid < N * N) m.A[tid] = sPA[G + tid];
+        if (tid == 0) record_iteration(m, sIn, L);
+    }
+    return cont;
 }
 
 // single-rank M-step with the statistics staged in dynamic LDS (copy_len doubles)
 __global__ void __launch_bounds__(256) k_mstep_staged(MArgs m) {
     extern __shared__ double sSt[];
-    if (m.state->done) return;
+    if (carry_if_done(m)) return;
     mstep_staged<false>(m, sSt);
-}
-
-// Fused M-step: the last E-step workgroup to finish (completion ticket) runs it.  Every value that
-// crosses workgroups inside the kernel (statistics copies, log-likelihood pairs, the ticket) moves
-// through memory-side atomics, so no per-XCD L2 can serve a stale line.
-__device__ void estep_tail(const EArgs &a, double *lds) {
-    __shared__ int last;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's atomics have completed
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        last = atomicAdd(a.ticket, 1u) == gridDim.x - 1;
-    }
-    __syncthreads();
-    if (!last) return;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    mstep_staged<true>(a.m, lds);
-    if (threadIdx.x == 0) atomicExch(a.ticket, 0u);
 }
 
 // safe_exp + normalisation of the returned parameters (:524-541)
@@ -1191,20 +1398,33 @@ struct hmmbw_ctx {
     std::vector<double> h_A;
     bool has_params = false;
     // training state
-    IterState *d_state = nullptr;
+    IterState *d_state = nullptr;  // [2]: the current slot is scur; every M-step writes the other
+    int scur = 0;
     double *d_hist = nullptr;
-    double *d_copies = nullptr;   // [ncopies][copy_len] E-step accumulators
-    unsigned *d_ticket = nullptr; // fused M-step completion counter
+    double *d_copies = nullptr;   // [3][ncopies][copy_len] E-step accumulators (iteration e uses e % 3)
     int ncopies = 1;
-    bool fuse_mstep = false;
+    bool merge_mstep = true;      // run each M-step in the prologue of the next E-step launch
     bool armed = false;
+    long long e_count = 0;        // E-step launches since the statistics were last cleared
+    // an M-step whose statistics are ready but which has not run yet (it runs in the next merged
+    // E-step launch, or on its own in flush_mstep before anything reads parameters or state)
+    struct Pending {
+        bool on = false;
+        bool local = true;        // statistics are this context's copies (single rank)
+        const double *src = nullptr;
+        int nsrc = 1;
+        const double *ll = nullptr;  // (max, sum exp) pairs of log P
+        long long nll = 0;
+        double *ext = nullptr;    // multi-rank: the caller's all-reduced buffer
+        long long R = 0;
+    } pend;
     // observations
     long long R = 0, nwaves = 0;
     long long nblocks = 0;
     uint16_t *d_sym = nullptr;
     long long *d_wsym = nullptr, *d_wckoff = nullptr, *d_wspoff = nullptr;
     int *d_wT = nullptr, *d_wfull = nullptr, *d_slen = nullptr, *d_sseq = nullptr;
-    double *d_ck = nullptr, *d_logp = nullptr, *d_llpart = nullptr;
+    double *d_ck = nullptr, *d_logp = nullptr, *d_llpart = nullptr;  // llpart: [2][nblocks][2]
     uint4 *d_sp = nullptr;
     int *d_ebuf = nullptr;
     bool has_obs = false;
@@ -1226,6 +1446,11 @@ struct hmmbw_ctx {
     long long copy_len() const { return off_ll(); }
     // emission table + B-numerator histogram in LDS ([K][G+1] fp64 each) when they fit 48 KiB
     bool lds_tables() const { return !wide && (size_t)(2 * K + 1) * (G + 1) * sizeof(double) <= 48 * 1024; }
+    // the merged M-step needs the LDS tables and the statistics in one register batch per thread
+    bool can_merge() const { return merge_mstep && lds_tables() && copy_len() <= kMergedMaxStats && nwaves > 0; }
+    IterState *state() const { return d_state + scur; }
+    double *copies(long long e) const { return d_copies + (e % 3) * (long long)ncopies * copy_len(); }
+    double *llpart(long long e) const { return d_llpart + (e % 2) * 2 * std::max(nblocks, 1LL); }
 };
 
 namespace {
@@ -1244,7 +1469,9 @@ void free_obs(hmmbw_ctx *c) {
 
 int realloc_stats(hmmbw_ctx *c) {
     dfree(c->d_copies);
-    const size_t n = (size_t)c->ncopies * c->copy_len();
+    c->pend.on = false;
+    c->e_count = 0;
+    const size_t n = 3 * (size_t)c->ncopies * c->copy_len();
     if (int rc = dalloc(&c->d_copies, n)) return rc;
     HIP_TRY(hipMemsetAsync(c->d_copies, 0, sizeof(double) * n, c->stream));
     return HMMBW_OK;
@@ -1260,14 +1487,14 @@ EArgs make_eargs(hmmbw_ctx *c) {
     a.ckpt = c->d_ck;
     a.spack = c->d_sp;
     a.ebuf = c->d_ebuf;
-    a.copies = c->d_copies;
+    a.copies = c->copies(0);
     a.copy_len = c->copy_len();
     a.ncopies = c->ncopies;
     a.logp = c->d_logp;
-    a.llpart = c->d_llpart;
+    a.llpart = c->llpart(0);
     a.force_safe = c->force_safe;
     a.ablate = c->ablate;
-    a.state = c->d_state;
+    a.state = c->state();
     a.K = c->K;
     a.N = c->N;
     a.off_S = c->off_S();
@@ -1277,27 +1504,29 @@ EArgs make_eargs(hmmbw_ctx *c) {
     return a;
 }
 
-// local: the statistics are this context's copies; otherwise the caller's all-reduced buffer
-MArgs make_margs(hmmbw_ctx *c, double *stats, long long R_global, bool local) {
+// M-step arguments for the pending statistics: this context's copies (single rank) or the caller's
+// all-reduced buffer with one (max, sum exp) pair per rank
+MArgs make_margs(hmmbw_ctx *c, const hmmbw_ctx::Pending &p) {
     MArgs m{};
-    m.src = local ? c->d_copies : stats;
-    m.zero_ll = local ? nullptr : stats + c->off_ll();
-    m.nsrc = local ? c->ncopies : 1;
+    m.src = p.src;
+    m.zero_ll = p.local ? nullptr : p.ext + c->off_ll();
+    m.nsrc = p.nsrc;
     m.copy_len = c->copy_len();
     m.pi = c->d_pi;
     m.A = c->d_A;
     m.B = c->d_B;
     m.Bt = c->d_Bt;
-    m.llpart = c->d_llpart;
-    m.nblocks = c->nblocks;
-    m.R_global = R_global;
-    m.state = c->d_state;
+    m.llpart = p.ll;
+    m.nblocks = p.nll;
+    m.R_global = p.R;
+    m.state = c->state();
+    m.state_out = c->d_state + (c->scur ^ 1);
     m.hist = c->d_hist;
     m.N = c->N;
     m.K = c->K;
     m.G = c->G;
     m.world = c->world;
-    m.local_lse = local ? 1 : 0;
+    m.local_lse = p.local ? 1 : 0;
     m.off_S = c->off_S();
     m.off_gex = c->off_gex();
     m.off_gall = c->off_gall();
@@ -1306,13 +1535,18 @@ MArgs make_margs(hmmbw_ctx *c, double *stats, long long R_global, bool local) {
     return m;
 }
 
-int launch_mstep(hmmbw_ctx *c, double *stats, long long R_global, bool local) {
+// run the pending M-step as its own one-workgroup kernel
+int flush_mstep(hmmbw_ctx *c) {
+    if (!c->pend.on) return HMMBW_OK;
+    c->pend.on = false;
+    const MArgs m = make_margs(c, c->pend);
     const size_t staged = sizeof(double) * (size_t)c->copy_len();
-    if (local && staged <= 64 * 1024 && c->N * c->N <= 256)
-        hipLaunchKernelGGL(k_mstep_staged, dim3(1), dim3(256), staged, c->stream, make_margs(c, stats, R_global, local));
+    if (m.local_lse && staged <= 64 * 1024 && c->N * c->N <= 256)
+        hipLaunchKernelGGL(k_mstep_staged, dim3(1), dim3(256), staged, c->stream, m);
     else
-        hipLaunchKernelGGL(k_mstep, dim3(1), dim3(256), 0, c->stream, make_margs(c, stats, R_global, local));
+        hipLaunchKernelGGL(k_mstep, dim3(1), dim3(256), 0, c->stream, m);
     HIP_TRY(hipGetLastError());
+    c->scur ^= 1;
     return HMMBW_OK;
 }
 
@@ -1326,23 +1560,25 @@ int launch_lds(F f, unsigned grid, size_t lds, hipStream_t stream, const EArgs &
     return HMMBW_OK;
 }
 
-// fuse: ask the last E-step workgroup to run the M-step (single rank); *fused reports whether it will
-int launch_estep(hmmbw_ctx *c, bool fwd_only, const IterState *state, bool fuse = false, bool *fused = nullptr) {
+// E-step launch e accumulates into copies and llpart; it clears `zero` (zero_len doubles) and, when
+// `merge` is set, first runs the pending M-step in its prologue (which consumes c->pend).
+int launch_estep(hmmbw_ctx *c, bool fwd_only, const IterState *state, double *copies = nullptr,
+                 double *llpart = nullptr, double *zero = nullptr, long long zero_len = 0, bool merge = false) {
     EArgs a = make_eargs(c);
     a.state = state;
+    if (copies) a.copies = copies;
+    if (llpart) a.llpart = llpart;
+    a.zero = zero;
+    a.zero_len = zero ? zero_len : 0;
     const int wpb = kBlock / kWave;
     const unsigned grid = (unsigned)((c->nwaves + wpb - 1) / wpb);
-    if (fused) *fused = false;
     if (grid == 0) return HMMBW_OK;
-    const size_t GPh = (size_t)c->G + 1;
-    const size_t lds_small = (c->lds_tables() ? ((size_t)c->K + 1) * GPh + (size_t)c->K * GPh : 0) +
-                             (size_t)wpb * c->G * ((c->topo == HMMBW_TOPOLOGY_LEFT_TO_RIGHT ? 2 : c->N) + 3) + 8;
-    if (fuse && !fwd_only && !c->wide && c->N * c->N <= 256 &&
-        (size_t)c->copy_len() <= std::max<size_t>(lds_small, 8192)) {
-        a.fused = 1;
-        a.ticket = c->d_ticket;
-        a.m = make_margs(c, nullptr, c->R, true);
-        if (fused) *fused = true;
+    bool flip = false;
+    if (merge && !fwd_only && c->pend.on && c->can_merge()) {
+        a.merged = 1;
+        a.m = make_margs(c, c->pend);
+        c->pend.on = false;
+        flip = true;  // the launch's M-step writes the other state slot
     }
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (c->timing && !fwd_only && (c->timing_seq++ % c->timing) == 0) {
@@ -1373,9 +1609,9 @@ int launch_estep(hmmbw_ctx *c, bool fwd_only, const IterState *state, bool fuse 
         const size_t GP = (size_t)c->G + 1;
         const size_t tabs = lds_tab ? ((size_t)c->K + 1) * GP + (fwd_only ? 0 : (size_t)c->K * GP) : 0;
         size_t lds = sizeof(double) * (tabs + (size_t)wpb * c->G * NV + 8);
-        if (a.fused) lds = std::max(lds, sizeof(double) * (size_t)c->copy_len());  // fused M-step staging
         if (int rc = launch_lds(f, grid, lds, c->stream, a)) return rc;
     }
+    if (flip) c->scur ^= 1;
     if (e1) {
         HIP_TRY(hipEventRecord(e1, c->stream));
         c->ev_pending.push_back(e0);
@@ -1455,13 +1691,12 @@ int hmmbw_ctx_create(int device, int n_states, int n_symbols, hmmbw_ctx **out) {
     if (!rc) rc = dalloc(&c->d_B, (size_t)c->N * c->K);
     if (!rc) rc = dalloc(&c->d_Bt, (size_t)c->K * c->G + c->G);
     if (!rc) rc = dalloc(&c->d_out, (size_t)c->N + (size_t)c->N * c->N + (size_t)c->N * c->K);
-    if (!rc) rc = dalloc(&c->d_state, 1);
-    if (!rc) rc = dalloc(&c->d_ticket, 1);
-    if (!rc && hipMemset(c->d_ticket, 0, sizeof(unsigned)) != hipSuccess) rc = fail(HMMBW_E_HIP, "ticket init");
+    if (!rc) rc = dalloc(&c->d_state, 2);
     if (!rc) rc = dalloc(&c->d_hist, 2 * (size_t)kHist);
     if (!rc) rc = realloc_stats(c);
     if (!rc) {
         hipLaunchKernelGGL(k_init_state, dim3(1), dim3(1), 0, c->stream, c->d_state, 0.0, 0LL);
+        hipLaunchKernelGGL(k_init_state, dim3(1), dim3(1), 0, c->stream, c->d_state + 1, 0.0, 0LL);
         hipError_t e = hipStreamSynchronize(c->stream);
         if (e != hipSuccess) rc = fail(HMMBW_E_HIP, std::string("init: ") + hipGetErrorString(e));
     }
@@ -1479,7 +1714,7 @@ int hmmbw_ctx_destroy(hmmbw_ctx *c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     else (void)hipDeviceSynchronize();
     dfree(c->d_pi); dfree(c->d_A); dfree(c->d_B); dfree(c->d_Bt); dfree(c->d_out);
-    dfree(c->d_state); dfree(c->d_hist); dfree(c->d_ticket); dfree(c->d_copies);
+    dfree(c->d_state); dfree(c->d_hist); dfree(c->d_copies);
     free_obs(c);
     for (auto e : c->ev_free) (void)hipEventDestroy(e);
     for (auto e : c->ev_pending) (void)hipEventDestroy(e);
@@ -1497,6 +1732,7 @@ int hmmbw_set_rank(hmmbw_ctx *c, int rank, int world) {
     if (!c) return fail(HMMBW_E_INVALID, "null context");
     if (world < 1 || rank < 0 || rank >= world) return fail(HMMBW_E_INVALID, "bad rank/world");
     if (int rc = set_device(c)) return rc;
+    if (int rc = flush_mstep(c)) return rc;
     c->rank = rank;
     c->world = world;
     return realloc_stats(c);
@@ -1539,6 +1775,7 @@ int hmmbw_set_observations(hmmbw_ctx *c, const int64_t *offsets, const int32_t *
             return fail(HMMBW_E_SYMBOL_RANGE, "symbol " + std::to_string(symbols[i]) + " at position " +
                                                   std::to_string(i) + " is outside [0, M)");
     if (int rc = set_device(c)) return rc;
+    if (int rc = flush_mstep(c)) return rc;      // it reads this layout's log-likelihood pairs
     HIP_TRY(hipStreamSynchronize(c->stream));  // buffers may still be in use by enqueued work
     // length-sorted (descending, stable) assignment of sequences to wave slots: the sequences that
     // share a wave have near-equal lengths, so the lockstep time loop wastes little
@@ -1609,7 +1846,7 @@ int hmmbw_set_observations(hmmbw_ctx *c, const int64_t *offsets, const int32_t *
         else rc = dalloc(&c->d_sp, (size_t)std::max(sptot, 1LL));
     }
     if (!rc) rc = dalloc(&c->d_logp, (size_t)std::max<int64_t>(R, 1));
-    if (!rc) rc = dalloc(&c->d_llpart, 2 * (size_t)std::max(nblocks, 1LL));
+    if (!rc) rc = dalloc(&c->d_llpart, 4 * (size_t)std::max(nblocks, 1LL));
     if (rc) return rc;
     HIP_TRY(hipMemcpy(c->d_sym, hsym.data(), sizeof(uint16_t) * hsym.size(), hipMemcpyHostToDevice));
     if (nwaves > 0) {
@@ -1623,7 +1860,7 @@ int hmmbw_set_observations(hmmbw_ctx *c, const int64_t *offsets, const int32_t *
     }
     std::vector<double> ninf((size_t)std::max<int64_t>(R, 1), -INFINITY);
     HIP_TRY(hipMemcpy(c->d_logp, ninf.data(), sizeof(double) * ninf.size(), hipMemcpyHostToDevice));
-    std::vector<double> zpairs(2 * (size_t)std::max(nblocks, 1LL), 0.0);
+    std::vector<double> zpairs(4 * (size_t)std::max(nblocks, 1LL), 0.0);
     HIP_TRY(hipMemcpy(c->d_llpart, zpairs.data(), sizeof(double) * zpairs.size(), hipMemcpyHostToDevice));
     c->R = R;
     c->nwaves = nwaves;
@@ -1641,12 +1878,15 @@ int hmmbw_set_option(hmmbw_ctx *c, int key, int64_t value) {
     if (key == HMMBW_OPT_STAT_COPIES) {
         if (value < 1 || value > 1024) return fail(HMMBW_E_INVALID, "statistics copies must be in [1, 1024]");
         if (int rc = set_device(c)) return rc;
+        if (int rc = flush_mstep(c)) return rc;
         HIP_TRY(hipStreamSynchronize(c->stream));
         c->ncopies = (int)value;
         return realloc_stats(c);
     }
-    if (key == HMMBW_OPT_FUSE_MSTEP) {
-        c->fuse_mstep = value != 0;
+    if (key == HMMBW_OPT_MERGE_MSTEP) {
+        if (int rc = set_device(c)) return rc;
+        if (int rc = flush_mstep(c)) return rc;
+        c->merge_mstep = value != 0;
         return HMMBW_OK;
     }
     if (key == HMMBW_OPT_ABLATE) {  // diagnostics: results are wrong while set
@@ -1659,6 +1899,7 @@ int hmmbw_set_option(hmmbw_ctx *c, int key, int64_t value) {
 int hmmbw_set_params(hmmbw_ctx *c, const double *pi, const double *A, const double *B) {
     if (!c || !pi || !A || !B) return fail(HMMBW_E_INVALID, "null argument");
     if (int rc = set_device(c)) return rc;
+    if (int rc = flush_mstep(c)) return rc;  // it would overwrite the new parameters later
     HIP_TRY(hipStreamSynchronize(c->stream));
     const int N = c->N, K = c->K, G = c->G;
     // safe_log semantics (hmm_training.py:46-54): x <= 0 (and NaN) is a zero probability
@@ -1685,9 +1926,11 @@ int hmmbw_set_params(hmmbw_ctx *c, const double *pi, const double *A, const doub
 int hmmbw_reset_training(hmmbw_ctx *c, double epsilon, int64_t max_iterations) {
     if (!c) return fail(HMMBW_E_INVALID, "null context");
     if (int rc = set_device(c)) return rc;
-    hipLaunchKernelGGL(k_init_state, dim3(1), dim3(1), 0, c->stream, c->d_state, epsilon, (long long)max_iterations);
+    if (int rc = flush_mstep(c)) return rc;
+    hipLaunchKernelGGL(k_init_state, dim3(1), dim3(1), 0, c->stream, c->state(), epsilon, (long long)max_iterations);
     HIP_TRY(hipGetLastError());
-    HIP_TRY(hipMemsetAsync(c->d_copies, 0, sizeof(double) * c->ncopies * c->copy_len(), c->stream));
+    HIP_TRY(hipMemsetAsync(c->d_copies, 0, sizeof(double) * 3 * c->ncopies * c->copy_len(), c->stream));
+    c->e_count = 0;
     c->armed = true;
     return HMMBW_OK;
 }
@@ -1701,11 +1944,16 @@ int hmmbw_stats_len(const hmmbw_ctx *c, int64_t *n) {
 int hmmbw_estep(hmmbw_ctx *c, double *stats_dev) {
     if (int rc = check_ready(c, true)) return rc;
     if (!stats_dev) return fail(HMMBW_E_INVALID, "null stats buffer");
-    if (int rc = launch_estep(c, false, c->d_state)) return rc;
+    if (c->pend.on && !c->can_merge())
+        if (int rc = flush_mstep(c)) return rc;
+    const long long e = c->e_count++;
+    double *llp = c->llpart(e);
+    // multi-rank: one copy set, cleared by k_reduce_local
+    if (int rc = launch_estep(c, false, c->state(), c->copies(0), llp, nullptr, 0, true)) return rc;
     const long long n = c->copy_len();
     const unsigned grid = (unsigned)std::min<long long>((n + 255) / 256, 64);
-    hipLaunchKernelGGL(k_reduce_local, dim3(grid), dim3(256), 0, c->stream, c->d_copies, c->ncopies, n, c->d_llpart,
-                       c->nblocks, stats_dev, c->off_ll(), c->world, c->rank, c->d_state);
+    hipLaunchKernelGGL(k_reduce_local, dim3(grid), dim3(256), 0, c->stream, c->copies(0), c->ncopies, n, llp,
+                       c->nblocks, stats_dev, c->off_ll(), c->world, c->rank, c->state());
     HIP_TRY(hipGetLastError());
     return HMMBW_OK;
 }
@@ -1713,17 +1961,43 @@ int hmmbw_estep(hmmbw_ctx *c, double *stats_dev) {
 int hmmbw_mstep(hmmbw_ctx *c, double *stats_dev, int64_t n_seq_global) {
     if (int rc = check_ready(c, true)) return rc;
     if (!stats_dev) return fail(HMMBW_E_INVALID, "null stats buffer");
-    return launch_mstep(c, stats_dev, n_seq_global, false);
+    if (int rc = flush_mstep(c)) return rc;
+    hmmbw_ctx::Pending &p = c->pend;
+    p.on = true;
+    p.local = false;
+    p.src = stats_dev;
+    p.nsrc = 1;
+    p.ll = stats_dev + c->off_ll();
+    p.nll = c->world;
+    p.ext = stats_dev;
+    p.R = n_seq_global;
+    // deferred into the next hmmbw_estep launch when that can merge it; queries flush it
+    return c->can_merge() ? HMMBW_OK : flush_mstep(c);
 }
 
 int hmmbw_iterate(hmmbw_ctx *c, int64_t n_iter) {
     if (int rc = check_ready(c, true)) return rc;
     if (c->world != 1) return fail(HMMBW_E_STATE, "hmmbw_iterate is single-rank; use estep/all-reduce/mstep");
+    const long long nz = (long long)c->ncopies * c->copy_len();
     for (int64_t i = 0; i < n_iter; ++i) {
-        bool fused = false;
-        if (int rc = launch_estep(c, false, c->d_state, c->fuse_mstep, &fused)) return rc;
-        if (!fused)
-            if (int rc = launch_mstep(c, nullptr, c->R, true)) return rc;
+        if (c->pend.on && !c->can_merge())
+            if (int rc = flush_mstep(c)) return rc;
+        const long long e = c->e_count++;
+        // statistics triple buffer: this launch adds into e, the merged M-step reads e - 1, and e + 1
+        // (read by launch e - 2) is cleared for the next launch
+        if (int rc = launch_estep(c, false, c->state(), c->copies(e), c->llpart(e), c->copies(e + 1), nz, true))
+            return rc;
+        hmmbw_ctx::Pending &p = c->pend;
+        p.on = true;
+        p.local = true;
+        p.src = c->copies(e);
+        p.nsrc = c->ncopies;
+        p.ll = c->llpart(e);
+        p.nll = c->nblocks;
+        p.ext = nullptr;
+        p.R = c->R;
+        if (!c->can_merge())
+            if (int rc = flush_mstep(c)) return rc;
         if (c->timing && c->ev_pending.size() >= 256)
             if (int rc = drain_timing(c)) return rc;
     }
@@ -1733,8 +2007,9 @@ int hmmbw_iterate(hmmbw_ctx *c, int64_t n_iter) {
 int hmmbw_get_status(hmmbw_ctx *c, hmmbw_status *st, hmmbw_iter_record *rec, int64_t first, int64_t count) {
     if (!c || !st) return fail(HMMBW_E_INVALID, "null argument");
     if (int rc = set_device(c)) return rc;
+    if (int rc = flush_mstep(c)) return rc;
     IterState h{};
-    HIP_TRY(hipMemcpyAsync(&h, c->d_state, sizeof(IterState), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(&h, c->state(), sizeof(IterState), hipMemcpyDeviceToHost, c->stream));
     std::vector<double> hist(2 * (size_t)kHist);
     if (rec && count > 0)
         HIP_TRY(hipMemcpyAsync(hist.data(), c->d_hist, sizeof(double) * hist.size(), hipMemcpyDeviceToHost, c->stream));
@@ -1760,6 +2035,7 @@ int hmmbw_get_params(hmmbw_ctx *c, double *pi, double *A, double *B, int normali
     if (!c || !pi || !A || !B) return fail(HMMBW_E_INVALID, "null argument");
     if (!c->has_params) return fail(HMMBW_E_STATE, "parameters not set");
     if (int rc = set_device(c)) return rc;
+    if (int rc = flush_mstep(c)) return rc;
     const size_t N = c->N, K = c->K;
     if (normalise) {
         hipLaunchKernelGGL(k_finalise, dim3(1), dim3(64), 0, c->stream, c->d_pi, c->d_A, c->d_B, c->N, c->K, c->d_out);
@@ -1789,6 +2065,7 @@ int hmmbw_get_loglik(hmmbw_ctx *c, double *out) {
 int hmmbw_score(hmmbw_ctx *c, double *out) {
     if (int rc = check_ready(c, false)) return rc;
     if (!out) return fail(HMMBW_E_INVALID, "null argument");
+    if (int rc = flush_mstep(c)) return rc;
     if (int rc = launch_estep(c, true, nullptr)) return rc;
     return hmmbw_get_loglik(c, out);
 }
@@ -1807,5 +2084,14 @@ int hmmbw_timing(hmmbw_ctx *c, int enable, double *total_ms, int64_t *count) {
     }
     return HMMBW_OK;
 }
+
+#ifdef HMMBW_PHASE_TIMES
+int hmmbw_debug_phase_times(unsigned long long *out, int64_t nwaves) {
+    if (!out || nwaves < 0 || nwaves > kPhaseWaves) return fail(HMMBW_E_INVALID, "bad argument");
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase), sizeof(unsigned long long) * 8 * nwaves));
+    return HMMBW_OK;
+}
+#endif
 
 }  // extern "C"

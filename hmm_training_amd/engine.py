@@ -18,7 +18,7 @@ from typing import Callable, List, Optional, Sequence, Tuple
 import numpy as np
 import torch
 
-from ._lib import OPT_FUSE_MSTEP, OPT_SAFE_SCALING, OPT_STAT_COPIES, TOPOLOGY, TOPOLOGY_NAME, IterRecord, Status, check, lib
+from ._lib import OPT_MERGE_MSTEP, OPT_SAFE_SCALING, OPT_STAT_COPIES, TOPOLOGY, TOPOLOGY_NAME, IterRecord, Status, check, lib
 
 IterCallback = Callable[[int, float, float], None]
 
@@ -61,14 +61,14 @@ def shard_bounds(lengths: Sequence[int], world: int) -> List[Tuple[int, int]]:
 
 class StatsLayout:
     """Packed fp64 statistics buffer of hmmbw_estep/hmmbw_mstep (include/hmmbw.h):
-    [pi_num N][S N*N][gamma_den_excl_last N][gamma_den_all N][B_num M*N (symbol-major)][(m, s) x world].
-    S_ij = sum_t alpha_hat_t(i) v_{t+1}(j), so the reference's xi numerator (hmm_training.py:443-455)
-    is a_ij * S_ij; (m, s) is a rank's (max_r log P_r, sum_r exp(log P_r - m)) pair."""
+    [pi_num N][xi N*N][gamma_den_excl_last N][gamma_den_all N][B_num M*N (symbol-major)][(m, s) x world].
+    xi_ij = sum_r sum_t xi_t(i, j), the linear form of the reference's xi numerator
+    (hmm_training.py:443-455); (m, s) is a rank's (max_r log P_r, sum_r exp(log P_r - m)) pair."""
 
     def __init__(self, N: int, M: int, world: int = 1):
         self.N, self.M, self.world = N, M, world
         self.pi = 0
-        self.S = N
+        self.xi = N
         self.gex = N + N * N
         self.gall = self.gex + N
         self.bnum = self.gall + N
@@ -78,7 +78,7 @@ class StatsLayout:
     def decode(self, buf: np.ndarray) -> dict:
         N, M = self.N, self.M
         buf = np.asarray(buf, dtype=np.float64)
-        return dict(pi_num=buf[: N], S=buf[self.S: self.S + N * N].reshape(N, N),
+        return dict(pi_num=buf[: N], xi=buf[self.xi: self.xi + N * N].reshape(N, N),
                     gamma_den_excl=buf[self.gex: self.gex + N], gamma_den_all=buf[self.gall: self.gall + N],
                     B_num=buf[self.bnum: self.bnum + M * N].reshape(M, N).T,
                     ll_pairs=buf[self.ll: self.ll + 2 * self.world].reshape(self.world, 2))
@@ -105,7 +105,7 @@ class BaumWelchEngine:
 
     def __init__(self, n_states: int, n_symbols: int, device: Optional[int] = None, topology: str = "auto",
                  rank: int = 0, world_size: int = 1, stream: Optional[int] = None, safe_scaling: bool = False,
-                 fuse_mstep: bool = False, stat_copies: int = 1):
+                 merge_mstep: bool = True, stat_copies: int = 1):
         self._lib = lib()
         self.N, self.M = int(n_states), int(n_symbols)
         self.device = default_device() if device is None else int(device)
@@ -122,8 +122,8 @@ class BaumWelchEngine:
         check(self._lib.hmmbw_set_topology(self._ctx, TOPOLOGY[topology]))
         if safe_scaling:
             check(self._lib.hmmbw_set_option(self._ctx, OPT_SAFE_SCALING, 1))
-        if fuse_mstep:
-            check(self._lib.hmmbw_set_option(self._ctx, OPT_FUSE_MSTEP, 1))
+        if not merge_mstep:
+            check(self._lib.hmmbw_set_option(self._ctx, OPT_MERGE_MSTEP, 0))
         if stat_copies != 1:
             check(self._lib.hmmbw_set_option(self._ctx, OPT_STAT_COPIES, int(stat_copies)))
         self.n_seq = 0

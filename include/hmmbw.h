@@ -94,18 +94,22 @@ int hmmbw_reset_training(hmmbw_ctx *ctx, double epsilon, int64_t max_iterations)
 int hmmbw_stats_len(const hmmbw_ctx *ctx, int64_t *n_doubles);
 
 /* E-step over this rank's sequences (hmm_training.py:351-410): writes this rank's packed statistics
- * {pi_num[N], S[N*N], gamma_den_excl_last[N], gamma_den_all[N], B_num[M*N], (m, s)[world]}
- * into the DEVICE buffer stats_dev (hmmbw_stats_len doubles; its (m, s) pair — the max and
- * sum-exp of log P_r — in slot `rank`, other slots zero).  Multi-rank callers all-reduce(sum)
- * stats_dev, then call hmmbw_mstep. */
+ * {pi_num[N], xi[N*N], gamma_den_excl_last[N], gamma_den_all[N], B_num[M*N], (m, s)[world]}
+ * (linear-domain sums: xi_ij = sum_r sum_t xi_t(i,j), B_num symbol-major [M][N]) into the DEVICE
+ * buffer stats_dev (hmmbw_stats_len doubles; its (m, s) pair — the max and sum-exp of log P_r —
+ * in slot `rank`, other slots zero).  Multi-rank callers all-reduce(sum) stats_dev, then call
+ * hmmbw_mstep.  A deferred M-step (below) runs at the start of this launch. */
 int hmmbw_estep(hmmbw_ctx *ctx, double *stats_dev);
 
 /* M-step + convergence (hmm_training.py:415-514) from the (all-reduced) statistics; n_seq_global
- * is the R of :424.  Zero-fills stats_dev for the next iteration.  No-op once done. */
+ * is the R of :424.  No-op once done.  With HMMBW_OPT_MERGE_MSTEP (default) it is DEFERRED: the
+ * next hmmbw_estep runs it in the prologue of its own kernel, so stats_dev must stay untouched until
+ * then; hmmbw_get_status / get_params / score / set_params / reset_training complete it first. */
 int hmmbw_mstep(hmmbw_ctx *ctx, double *stats_dev, int64_t n_seq_global);
 
-/* Single-rank fused loop: enqueue n_iter iterations of (estep, mstep) with internal statistics.
- * Iterations after convergence are device-side no-ops (same result as stopping, :346). */
+/* Single-rank loop: enqueue n_iter iterations of (estep, mstep) with internal statistics (the last
+ * M-step stays deferred until a query, as for hmmbw_mstep).  Iterations after convergence are
+ * device-side no-ops (same result as stopping, :346). */
 int hmmbw_iterate(hmmbw_ctx *ctx, int64_t n_iter);
 
 /* SYNC. Status plus the iteration records [first, first+count) (ring of 4096 entries). */
@@ -134,9 +138,10 @@ int hmmbw_score(hmmbw_ctx *ctx, double *out);
 /* Number of statistics accumulator copies the E-step's workgroups spread their atomics over
  * (workgroup b adds into copy b % n; default 1). */
 #define HMMBW_OPT_STAT_COPIES 3
-/* 1: hmmbw_iterate runs the M-step in the last E-step workgroup to finish instead of a second
- * kernel (cross-workgroup data through memory-side atomics).  Default 0. */
-#define HMMBW_OPT_FUSE_MSTEP 4
+/* 1 (default): every M-step runs in the prologue of the next E-step launch, computed redundantly by
+ * each workgroup straight into its LDS tables (when the emission tables fit LDS); 0: a separate
+ * one-workgroup M-step kernel after every E-step. */
+#define HMMBW_OPT_MERGE_MSTEP 4
 int hmmbw_set_option(hmmbw_ctx *ctx, int key, int64_t value);
 
 /* E-step kernel timing with HIP events on the context stream (for bench/roofline).  Returns the

@@ -29,9 +29,7 @@ def packed_stats(offsets, symbols, N, M, pi, A, B, world, rank):
     if len(offsets) > 1:
         s = O.estep_logstats(offsets, symbols, N, M, pi, A, B)
         buf[L.pi:L.pi + N] = np.exp(s.log_pi_num)
-        with np.errstate(divide="ignore", invalid="ignore"):
-            S = np.where(A > 0, np.exp(s.log_xi) / np.where(A > 0, A, 1.0), 0.0)
-        buf[L.S:L.S + N * N] = S.reshape(-1)
+        buf[L.xi:L.xi + N * N] = np.exp(s.log_xi).reshape(-1)
         buf[L.gex:L.gex + N] = np.exp(s.log_gden_excl)
         buf[L.gall:L.gall + N] = np.exp(s.log_gden_all)
         buf[L.bnum:L.bnum + M * N] = np.exp(s.log_bnum).T.reshape(-1)
@@ -86,7 +84,7 @@ def test_sharded_stats_allreduce_equals_single_rank(world, case, tmp_path, oracl
     Lw = StatsLayout(N, M, world)
     red = Lw.decode(outs[0])
     ref = L1.decode(full)
-    for key in ("pi_num", "S", "gamma_den_excl", "gamma_den_all", "B_num"):
+    for key in ("pi_num", "xi", "gamma_den_excl", "gamma_den_all", "B_num"):
         np.testing.assert_allclose(red[key], ref[key], rtol=1e-12, atol=1e-300)
     # global convergence scalar from the per-rank slots == the reference's LSE over all log P
     lp = oracle.estep_logstats(d["offsets"], d["symbols"], N, M, d["init_pi"], d["init_A"], d["init_B"]).logP

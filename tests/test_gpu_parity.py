@@ -181,7 +181,7 @@ def test_estep_statistics_vs_oracle(topology, oracle):
         got = StatsLayout(N, K).decode(stats.cpu().numpy())
         assert_ll(eng.loglik(), s.logP)
     np.testing.assert_allclose(got["pi_num"], np.exp(s.log_pi_num), rtol=1e-9, atol=1e-300)
-    np.testing.assert_allclose(A * got["S"], np.exp(s.log_xi), rtol=1e-9, atol=1e-300)
+    np.testing.assert_allclose(got["xi"], np.exp(s.log_xi), rtol=1e-9, atol=1e-300)
     np.testing.assert_allclose(got["gamma_den_excl"], np.exp(s.log_gden_excl), rtol=1e-9)
     np.testing.assert_allclose(got["gamma_den_all"], np.exp(s.log_gden_all), rtol=1e-9)
     np.testing.assert_allclose(got["B_num"], np.exp(s.log_bnum), rtol=1e-9, atol=1e-300)
@@ -214,7 +214,7 @@ def test_full_size_cfg3_properties(oracle):
         ll = eng.loglik()
     assert np.all(np.isfinite(ll))
     np.testing.assert_allclose(g["B_num"].sum(1), g["gamma_den_all"], rtol=1e-11)
-    np.testing.assert_allclose((A * g["S"]).sum(1), g["gamma_den_excl"], rtol=1e-11)
+    np.testing.assert_allclose(g["xi"].sum(1), g["gamma_den_excl"], rtol=1e-11)
     assert np.isclose(g["pi_num"].sum(), R, rtol=1e-12)
     assert np.isclose(g["gamma_den_all"].sum(), R * T, rtol=1e-12)
     pick = rng.choice(R, size=48, replace=False)
@@ -305,14 +305,14 @@ def test_pathological_emissions_fall_back_to_safe_scaling(topology, equal_length
     assert_params(p2, ref.pi, "pi")
 
 
-@pytest.mark.parametrize("fuse,copies", [(True, 1), (True, 4), (False, 4)])
+@pytest.mark.parametrize("merge,copies", [(True, 4), (False, 1), (False, 4)])
 @pytest.mark.parametrize("case", ["n8_k256_cfg2", "n4_k16_default", "converge", "dense_n6"])
-def test_engine_variants_match_reference(case, fuse, copies):
-    """The fused-M-step and multi-copy accumulation variants give the reference's results."""
+def test_engine_variants_match_reference(case, merge, copies):
+    """The separate-M-step-kernel and multi-copy accumulation variants give the reference's results."""
     from hmm_training_amd.engine import BaumWelchEngine
     d = load(case)
     N, M = int(d["N"]), int(d["M"])
-    with BaumWelchEngine(N, M, fuse_mstep=fuse, stat_copies=copies) as eng:
+    with BaumWelchEngine(N, M, merge_mstep=merge, stat_copies=copies) as eng:
         eng.set_observations(observations(d))
         eng.set_params(d["init_pi"], d["init_A"], d["init_B"])
         trace = []

@@ -1,0 +1,80 @@
+#!/usr/bin/env python3
+"""Per-wave phase timeline of the small E-step (diagnostics).
+
+Builds an instrumented copy of the engine (-DHMMBW_PHASE_TIMES) into gpurun_out/, runs the bench
+workload for a few iterations and prints, for the last launch, the distribution over waves of each
+phase's duration and of the phase boundaries relative to the earliest wave start (wall clock, 100 MHz).
+
+    python tools/phase_times.py [--R 10000] [--topology left_to_right] [--no-merge]
+"""
+import argparse
+import ctypes
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--R", type=int, default=10000)
+    ap.add_argument("--T", type=int, default=200)
+    ap.add_argument("--N", type=int, default=8)
+    ap.add_argument("--K", type=int, default=256)
+    ap.add_argument("--topology", default="left_to_right")
+    ap.add_argument("--no-merge", action="store_true")
+    ap.add_argument("--iters", type=int, default=6)
+    a = ap.parse_args()
+    out_dir = os.path.join(ROOT, "gpurun_out", "phase")
+    os.makedirs(out_dir, exist_ok=True)
+    lib = os.path.join(out_dir, "libhmmbw_phase.so")
+    from hmm_training_amd import build as B
+    subprocess.run([B.HIPCC, *B.FLAGS, "-DHMMBW_PHASE_TIMES", B.SRC, "-o", lib], check=True)
+    os.environ["HMMBW_LIB"] = lib
+    import torch
+    from hmm_training_amd.engine import BaumWelchEngine
+    from hmm_training_amd.hmm_training import default_initial_params
+    R, T, N, K = a.R, a.T, a.N, a.K
+    rng = np.random.default_rng(3)
+    sym = rng.integers(0, K, size=R * T).astype(np.int32)
+    pi, A, Bm = default_initial_params(N, K)
+    if a.topology == "dense":
+        A = 0.5 * A + 0.5 * rng.dirichlet(np.ones(N), size=N)
+    eng = BaumWelchEngine(N, K, topology=a.topology, merge_mstep=not a.no_merge)
+    eng.set_observations(offsets=np.arange(R + 1, dtype=np.int64) * T, symbols=sym)
+    eng.set_params(pi, A, Bm)
+    eng.reset(0.0, a.iters + 1)
+    eng.enqueue_iterations(a.iters)
+    torch.cuda.synchronize()
+    U = 64 // (1 << max(1, (N - 1).bit_length()))
+    nw = (R + U - 1) // U
+    nw_pad = ((nw + 3) // 4) * 4
+    buf = np.zeros((nw_pad, 8), dtype=np.uint64)
+    l = eng._lib
+    l.hmmbw_debug_phase_times.argtypes = [ctypes.c_void_p, ctypes.c_int64]
+    rc = l.hmmbw_debug_phase_times(buf.ctypes.data, nw_pad)
+    assert rc == 0, rc
+    t = buf[:nw].astype(np.int64)
+    t0 = t[:, 0].min()
+    us = lambda x: x / 100.0  # 100 MHz wall clock -> us
+    names = ["start", "tables", "forward", "backward", "ll", "flush"]
+    print(f"waves {nw}  kernel span {us(t[:, 5].max() - t0):.2f} us")
+    for k in range(1, 6):
+        d = us(t[:, k] - t[:, k - 1])
+        print(f"{names[k-1]:>8s}->{names[k]:<8s} mean {d.mean():7.2f}  p50 {np.median(d):7.2f}  max {d.max():7.2f} us")
+    for k in range(6):
+        r = us(t[:, k] - t0)
+        print(f"at {names[k]:<8s} rel-start  min {r.min():7.2f}  p50 {np.median(r):7.2f}  max {r.max():7.2f} us")
+    if np.all(t[:, 6] > 0):  # merged M-step prologue: statistics gathered / tables built
+        for k, nm in ((6, "mstep-loads"), (7, "mstep-tables")):
+            r = us(t[:, k] - t0)
+            print(f"at {nm:<12s} rel-start  min {r.min():7.2f}  p50 {np.median(r):7.2f}  max {r.max():7.2f} us")
+    np.save(os.path.join(out_dir, "phase_nomerge.npy" if a.no_merge else "phase_merge.npy"), t)
+
+
+if __name__ == "__main__":
+    main()
