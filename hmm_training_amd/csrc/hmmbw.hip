@@ -55,7 +55,17 @@ __device__ unsigned long long g_phase[kPhaseWaves][8];
         const long long w_ = (long long)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);   \
         if ((threadIdx.x & 63) == 0 && w_ < kPhaseWaves) g_phase[w_][k] = wall_clock64();      \
     } while (0)
+// shader-clock stamp at the start of forward (d = 0) / backward (d = 1) chunk c (c < 64)
+__device__ unsigned long long g_chunk[4096][2][64];
+#define CHUNKSTAMP(d, c)                                                                       \
+    do {                                                                                       \
+        const long long w_ = (long long)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);   \
+        if ((threadIdx.x & 63) == 0 && w_ < 4096 && (c) < 64) g_chunk[w_][d][c] = clock64();   \
+    } while (0)
 #else
+#define CHUNKSTAMP(d, c) \
+    do {                 \
+    } while (0)
 #define PHASE(k) \
     do {         \
     } while (0)
@@ -271,8 +281,8 @@ __device__ void block_ll_partial(double lp, bool valid, double *sh, double *out)
 //   gamma_t(i) = z_t(i) beta_hat_t(i),  xi_t(i,j) = a_ij z_t(i) v_j  (accumulated as S_ij = xi/a_ij).
 // gamma is scattered into the per-workgroup LDS histogram B_num[o_t][j] (ds_add_f64).
 // ---------------------------------------------------------------------------------------------
-template <int N, int G, int GP, bool HIST>
-__device__ bool merged_mstep(const EArgs &a, double *sBt, double *sBn, double *sPA);
+template <int N, int G, int GP, bool HIST, bool PT>
+__device__ bool merged_mstep(const EArgs &a, double *sBt, double2 *sBP, double *sBn, double *sPA);
 
 template <int N, int G, bool LR, bool LDSTAB, bool FWD_ONLY>
 __global__ void __launch_bounds__(kBlock) k_estep_small(EArgs a) {
@@ -280,6 +290,8 @@ __global__ void __launch_bounds__(kBlock) k_estep_small(EArgs a) {
     constexpr int NS = LR ? 2 : N;      // per-lane S accumulators (row j of S)
     constexpr int NV = NS + 3;          // + gamma_den_excl, gamma_den_all, pi_num
     constexpr int GP = LDSTAB ? G + 1 : G;  // row stride of the emission / histogram tables
+    // left-to-right with LDS tables: per (symbol, state) products {a_jj b_j(o), a_{j-1,j} b_j(o)}
+    constexpr bool PT = LR && LDSTAB;
     extern __shared__ double smem[];
     __shared__ double sPA[G + N * N];  // pi (zero-padded to G) and A of this iteration
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -290,8 +302,10 @@ __global__ void __launch_bounds__(kBlock) k_estep_small(EArgs a) {
             a.zero[i] = 0.0;
     const int j = lane & (G - 1), u = lane / G;
     const int K = a.K;
-    double *sBt = smem;                                               // [K][GP] + pad
-    double *sBn = smem + (LDSTAB ? (size_t)K * GP + GP : 0);          // [K][GP]
+    const size_t ntab = LDSTAB ? (((size_t)K + 1) * GP + 1) & ~(size_t)1 : 0;  // even: 16-B alignment
+    double *sBt = smem;                                               // [K+1][GP] b_j(o)
+    double2 *sBP = reinterpret_cast<double2 *>(smem + ntab);          // PT: [K+1][GP] products
+    double *sBn = smem + ntab + (PT ? 2 * ntab : 0);                  // [K][GP] B numerator histogram
     double *sRed = sBn + ((LDSTAB && !FWD_ONLY) ? (size_t)K * GP : 0); // [waves][G][NV] + ll scratch
     bool merged = false;
     if constexpr (LDSTAB && !FWD_ONLY) merged = a.merged != 0;
@@ -299,7 +313,7 @@ __global__ void __launch_bounds__(kBlock) k_estep_small(EArgs a) {
         // the previous iteration's M-step, computed redundantly by every workgroup straight into
         // its LDS tables (no separate M-step kernel, no parameter round trip through HBM)
         if constexpr (LDSTAB && !FWD_ONLY)
-            if (!merged_mstep<N, G, GP, true>(a, sBt, sBn, sPA)) return;  // done or stopped (:346)
+            if (!merged_mstep<N, G, GP, true, PT>(a, sBt, sBP, sBn, sPA)) return;  // done or stopped (:346)
     } else {
         if (a.state != nullptr && a.state->done) return;  // converged: device-side no-op
         if (tid < G) sPA[tid] = tid < N ? a.pi[tid] : 0.0;
@@ -330,6 +344,16 @@ __global__ void __launch_bounds__(kBlock) k_estep_small(EArgs a) {
             }
         }
         __syncthreads();
+        if constexpr (PT) {
+            for (int i = tid; i < (K + 1) * GP; i += kBlock) {
+                const int c = i % GP;
+                const double b = sBt[i];
+                const double ad = c < N ? sPA[G + c * N + c] : 0.0;
+                const double ai = (c >= 1 && c < N) ? sPA[G + (c - 1) * N + c] : 0.0;
+                sBP[i] = double2{ad * b, ai * b};
+            }
+            __syncthreads();
+        }
     }
     const double *Btab = LDSTAB ? sBt : a.Bt;
     PHASE(1);
@@ -376,19 +400,33 @@ __global__ void __launch_bounds__(kBlock) k_estep_small(EArgs a) {
             return *reinterpret_cast<const uint4 *>(symw + (long long)c * U * kChunk);
         };
         // Emission-table element of this lane for packed entry k.  With LDS tables the packs hold the
-        // byte offset of the symbol's row (o * GP * 8, precomputed on the host), else the symbol.
+        // byte offset of the symbol's row in the 16-byte product table (o * GP * 16, precomputed on
+        // the host; half of it in the 8-byte tables), else the symbol.
         const char *tabj = reinterpret_cast<const char *>(Btab + j);
         auto brow = [&](const uint4 &p, int k) -> const double * {
-            if constexpr (LDSTAB) return reinterpret_cast<const double *>(tabj + sym_of(p, k));
+            if constexpr (LDSTAB) return reinterpret_cast<const double *>(tabj + (sym_of(p, k) >> 1));
             else return reinterpret_cast<const double *>(tabj) + (size_t)sym_of(p, k) * GP;
         };
-        // One forward step: (A^T z_{t-1})_j * bs, bs = b_j(o_t) [* 2^-s_t].  Used verbatim by the
-        // forward sweep and by the backward recompute, so both produce bit-identical z_t.
-        auto step = [&](double zp, double bs) -> double {
-            if constexpr (LR) {
+        // the emission operand of one step: the product pair (PT) or b_j(o)
+        using Em = typename std::conditional<PT, double2, double>::type;
+        const char *tabPj = reinterpret_cast<const char *>(sBP + j);
+        auto ld_em = [&](const uint4 &p, int k) -> Em {
+            if constexpr (PT) return *reinterpret_cast<const double2 *>(tabPj + sym_of(p, k));
+            else return *brow(p, k);
+        };
+        // One forward step (hmm_training.py:122-160 without the 2^-s rescale, which the caller
+        // applies): PT  a_jj b_j z_{t-1}(j) + a_{j-1,j} b_j z_{t-1}(j-1);  LR  the same from a and b;
+        // dense  (A^T z_{t-1})_j b_j.  Used verbatim by the forward sweep and the backward recompute,
+        // so both produce bit-identical z_t.
+        auto step = [&](double zp, Em e) -> double {
+            if constexpr (PT) {
+                const double prev = dpp<0x111>(zp);  // row_shr:1 -> z_{t-1}(j-1); 0 in lane 0 of a group
+                return fma(e.y, prev, e.x * zp);
+            } else if constexpr (LR) {
                 const double prev = dpp<0x111>(zp);  // row_shr:1 -> z_{t-1}(j-1); a_in = 0 for j = 0
-                return fma(a_in * bs, prev, (a_dg * bs) * zp);
+                return fma(a_in * e, prev, (a_dg * e) * zp);
             } else {
+                const double bs = e;
                 double acc0 = 0.0, acc1 = 0.0;
                 sfor<0, N>([&](auto I) {
                     const double zi = gbcast<G, I.value>(zp, lane);
@@ -417,12 +455,18 @@ __global__ void __launch_bounds__(kBlock) k_estep_small(EArgs a) {
             C = 0;
             int pend[kChunk / kScale] = {};  // lagged: exponents to apply at the coming scale steps
             int minM = 4096, maxM = 0;       // extreme group exponents seen (fallback trigger)
-            uint4 p0 = loadpack(0);
-            uint4 p1 = nch > 1 ? loadpack(1) : p0;
-            double bv[kChunk];
+            // Symbol packs travel through a 4-deep register ring (the pack of chunk c + 4 is loaded
+            // while chunk c runs) and the emissions through a 2-deep one (chunk c + 1's LDS reads are
+            // issued before chunk c computes); the sweep is unrolled by 4 so no ring slot is ever
+            // copied, which would wait on the load that just filled it.
+            uint4 Q[4];
 #pragma unroll
-            for (int k = 0; k < kChunk; ++k) bv[k] = *brow(p0, k);
-            auto chunk = [&](int c, auto MASK_) {
+            for (int i = 0; i < 4; ++i) Q[i] = loadpack(i < nch ? i : nch - 1);
+            const double b00 = *brow(Q[0], 0);  // b_j(o_0) for pi_j b_j(o_0) (:357-360)
+            Em E[2][kChunk];
+#pragma unroll
+            for (int k = 0; k < kChunk; ++k) E[0][k] = ld_em(Q[0], k);
+            auto chunk = [&](int c, const Em (&bv)[kChunk], auto MASK_) {
                 constexpr bool MASK = decltype(MASK_)::value;
                 const int Tend = RAG ? T : Tw;
                 int sp[kChunk];
@@ -432,14 +476,13 @@ __global__ void __launch_bounds__(kBlock) k_estep_small(EArgs a) {
                     double zn;
                     int st = 0;
                     if constexpr (SAFE) {
-                        const double x = (t == 0) ? pij * bv[k] : step(z, bv[k]);
+                        const double x = (t == 0) ? pij * b00 : step(z, bv[k]);
                         const int M = group_bexp(x);
                         st = M == 0 ? 0 : M - 1023;
                         zn = pow2_scale(x, st);
                     } else if (k % kScale == 0) {
                         st = pend[k / kScale];
-                        const double bs = pow2_scale(bv[k], st);
-                        zn = (t == 0) ? pij * bs : step(z, bs);
+                        zn = pow2_scale((t == 0) ? pij * b00 : step(z, bv[k]), st);
                         const int M = group_bexp(zn);
                         // applied kScale steps later; clamped so an all-zero (dead) group can never
                         // scale itself to inf (the fallback below catches it)
@@ -465,17 +508,20 @@ __global__ void __launch_bounds__(kBlock) k_estep_small(EArgs a) {
                 }
                 if constexpr (!FWD_ONLY) spw[(long long)c * U] = pack_exps(sp);
             };
-            for (int c = 0; c < nch; ++c) {
-                const uint4 p2 = (c + 2 < nch) ? loadpack(c + 2) : p1;
-                double bvn[kChunk];  // next chunk's emissions, in flight during this chunk
+            auto body = [&](int c, auto R_) {
+                constexpr int r = decltype(R_)::value;
+                CHUNKSTAMP(0, c);
 #pragma unroll
-                for (int k = 0; k < kChunk; ++k) bvn[k] = *brow(p1, k);
-                if (RAG || (c == nch - 1 && (Tw % kChunk) != 0)) chunk(c, std::true_type{});
-                else chunk(c, std::false_type{});
-#pragma unroll
-                for (int k = 0; k < kChunk; ++k) bv[k] = bvn[k];
-                p0 = p1;
-                p1 = p2;
+                for (int k = 0; k < kChunk; ++k) E[(r + 1) & 1][k] = ld_em(Q[(r + 1) & 3], k);
+                if (c + 4 < nch) Q[r] = loadpack(c + 4);
+                if (RAG || (c == nch - 1 && (Tw % kChunk) != 0)) chunk(c, E[r & 1], std::true_type{});
+                else chunk(c, E[r & 1], std::false_type{});
+            };
+            for (int c = 0; c < nch; c += 4) {
+                body(c, std::integral_constant<int, 0>{});
+                if (c + 1 < nch) body(c + 1, std::integral_constant<int, 1>{});
+                if (c + 2 < nch) body(c + 2, std::integral_constant<int, 2>{});
+                if (c + 3 < nch) body(c + 3, std::integral_constant<int, 3>{});
             }
             return (!SAFE) && (minM < 1023 - 900 || maxM > 1023 + 900);
         };
@@ -507,46 +553,65 @@ __global__ void __launch_bounds__(kBlock) k_estep_small(EArgs a) {
                 constexpr bool RAG = decltype(RAG_)::value;
                 double beta = inv_p;
                 const int cl = (Tw - 1) / kChunk;
-                auto ldck = [&](int c) { return ckw[(long long)c * kWave]; };
-                auto ldsp = [&](int c) { return spw[(long long)c * U]; };
-                double ckA = ldck(cl), ckB = ldck(cl >= 1 ? cl - 1 : 0);
-                uint4 spA = ldsp(cl), spB = ldsp(cl >= 1 ? cl - 1 : 0);
-                uint4 pkA = loadpack(cl), pkB = loadpack(cl >= 1 ? cl - 1 : 0);
-                double bv[kChunk], bu[kChunk];
-                auto ldrows = [&](const uint4 &p) {
+                // per-chunk inputs (checkpoint, scale exponents, symbol pack) through a 4-deep register
+                // ring: chunk c - 4's are loaded as soon as chunk c is done with its slot; emissions
+                // through a 2-deep one; unrolled by 4 so no slot is copied (see the forward)
+                struct Ld {
+                    double ck;
+                    uint4 sp, pk;
+                };
+                auto ldset = [&](int c) -> Ld {
+                    return Ld{ckw[(long long)c * kWave], spw[(long long)c * U], loadpack(c)};
+                };
+                Ld X[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) X[i] = ldset(cl - i >= 0 ? cl - i : 0);
+                Em E[2][kChunk];
+                double BU[2][kChunk];
+                auto ldrows = [&](Em (&bv)[kChunk], double (&bu)[kChunk], const uint4 &p) {
 #pragma unroll
                     for (int k = 0; k < kChunk; ++k) {
-                        const double *r = brow(p, k);
-                        bv[k] = r[0];
-                        if constexpr (LR) bu[k] = r[1];  // b_{j+1}(o): the neighbour's emission
+                        if constexpr (PT) {
+                            bv[k] = ld_em(p, k);
+                        } else {
+                            const double *r = brow(p, k);
+                            bv[k] = r[0];
+                            if constexpr (LR) bu[k] = r[1];  // b_{j+1}(o): the neighbour's emission
+                        }
                     }
                 };
-                ldrows(pkA);
+                ldrows(E[0], BU[0], X[0].pk);
                 double f_hi = 0.0, fu_hi = 0.0;  // scaled emissions at o_{8c+8} (from chunk c+1)
-                auto chunk = [&](int c, auto MASK_) {
+                Em e_hi{};                       // PT: product pair at o_{8c+8} ...
+                int s_hi = 0;                    // ... and that step's scale exponent
+                auto chunk = [&](int c, const Ld &cur, const uint4 &pkn, const Em (&bv)[kChunk],
+                                 const double (&bu)[kChunk], Em (&bvn)[kChunk], double (&bun)[kChunk],
+                                 auto MASK_) {
                     constexpr bool MASK = decltype(MASK_)::value;
+                    const uint4 &spA = cur.sp, &pkA = cur.pk;
                     int sk[kChunk];
-                    double fs[kChunk], fus[kChunk];  // b(o_t) / c_t for t = 8c .. 8c+7
+                    double fs[kChunk], fus[kChunk];  // non-PT: b(o_t) / c_t for t = 8c .. 8c+7
 #pragma unroll
                     for (int k = 0; k < kChunk; ++k) {
                         const bool scaled = SAFE || (k % kScale == 0);
                         sk[k] = scaled ? exp_of(spA, k) : 0;
-                        fs[k] = scaled ? pow2_scale(bv[k], sk[k]) : bv[k];
-                        if constexpr (LR) fus[k] = scaled ? pow2_scale(bu[k], sk[k]) : bu[k];
+                        if constexpr (!PT) {
+                            fs[k] = scaled ? pow2_scale(bv[k], sk[k]) : bv[k];
+                            if constexpr (LR) fus[k] = scaled ? pow2_scale(bu[k], sk[k]) : bu[k];
+                        }
                     }
                     // recompute z_{8c .. 8c+7} from the checkpoint (identical ops to the forward)
                     double zr[kChunk];
-                    zr[0] = ckA;
+                    zr[0] = cur.ck;
 #pragma unroll
                     for (int k = 1; k < kChunk; ++k) {
-                        if constexpr (SAFE) zr[k] = pow2_scale(step(zr[k - 1], bv[k]), sk[k]);
-                        else zr[k] = step(zr[k - 1], fs[k]);
+                        const double x = step(zr[k - 1], bv[k]);
+                        zr[k] = (SAFE || (k % kScale == 0)) ? pow2_scale(x, sk[k]) : x;
                     }
                     double gk[kChunk];
 #pragma unroll
                     for (int k = kChunk - 1; k >= 0; --k) {
                         const int t = c * kChunk + k;
-                        const double f = (k == kChunk - 1) ? f_hi : fs[k + 1];  // b(o_{t+1}) / c_{t+1}
                         const double zt = zr[k];
                         // regular step (t <= T-2) / gamma_{T-1} (t == T-1) / past the end; per lane in
                         // ragged waves, wave-uniform otherwise; only boundary chunks are masked.
@@ -555,7 +620,22 @@ __global__ void __launch_bounds__(kBlock) k_estep_small(EArgs a) {
                         const bool ini = MASK && (RAG ? (t == T - 1) : (t == Tw - 1));
                         const double zs = reg ? zt : 0.0;
                         double bn;
-                        if constexpr (LR) {
+                        if constexpr (PT) {
+                            // beta_hat_t(j) = a_jj b_j(o') beta'(j) + a_j,j+1 b_j+1(o') beta'(j+1) with
+                            // beta' = beta_hat_{t+1} / c_{t+1} (:163-199); the second term is the
+                            // neighbour's a_{j,j+1} b_{j+1} beta' product, shifted down one lane (zero
+                            // past the last state: a_{N-1,N} does not exist, Bi(., 0) = 0)
+                            const Em e = (k == kChunk - 1) ? e_hi : bv[k + 1];
+                            const int s1 = (k == kChunk - 1) ? s_hi : sk[(k + 1) & (kChunk - 1)];
+                            const bool sc1 = SAFE || ((k + 1) % kScale == 0);
+                            const double bp = sc1 ? pow2_scale(beta, s1) : beta;
+                            const double vd = e.x * bp;
+                            const double vu = dpp<0x101>(e.y * bp);  // row_shl:1
+                            bn = vd + vu;
+                            S[0] = fma(zs, vd, S[0]);  // xi_t(j,j)   (:396-410)
+                            S[1] = fma(zs, vu, S[1]);  // xi_t(j,j+1)
+                        } else if constexpr (LR) {
+                            const double f = (k == kChunk - 1) ? f_hi : fs[k + 1];  // b(o_{t+1}) / c_{t+1}
                             const double fu = (k == kChunk - 1) ? fu_hi : fus[k + 1];
                             const double bup = dpp<0x101>(beta);  // row_shl:1 -> beta(j+1)
                             const double vd = f * beta, vu = fu * bup;
@@ -563,6 +643,7 @@ __global__ void __launch_bounds__(kBlock) k_estep_small(EArgs a) {
                             S[0] = fma(zs, vd, S[0]);             // xi_t(j,j)   / a_jj
                             S[1] = fma(zs, vu, S[1]);             // xi_t(j,j+1) / a_j,j+1 (scaled at the end)
                         } else {
+                            const double f = (k == kChunk - 1) ? f_hi : fs[k + 1];  // b(o_{t+1}) / c_{t+1}
                             const double vd = f * beta;
                             double b0 = 0.0, b1 = 0.0;
                             sfor<0, N>([&](auto I) {
@@ -587,30 +668,42 @@ __global__ void __launch_bounds__(kBlock) k_estep_small(EArgs a) {
                         if (t == 0) pin = g;  // :420
                         gk[k] = g;
                     }
+                    if constexpr (PT) {
+                        e_hi = bv[0];
+                        s_hi = sk[0];
+                    }
                     // next chunk's emission rows go to LDS before this chunk's histogram atomics, so
                     // they are not queued behind them
-                    ldrows(pkB);
+                    ldrows(bvn, bun, pkn);
                     if ((N == G || jv) && !(a.ablate & 4)) {
 #pragma unroll
                         for (int k = 0; k < kChunk; ++k) {  // :474-485
                             if constexpr (LDSTAB) {
-                                atomicAdd(reinterpret_cast<double *>(reinterpret_cast<char *>(sBn + j) + sym_of(pkA, k)), gk[k]);
+                                atomicAdd(reinterpret_cast<double *>(reinterpret_cast<char *>(sBn + j) + (sym_of(pkA, k) >> 1)), gk[k]);
                             } else if (gk[k] != 0.0) {
                                 unsafeAtomicAdd(&accb[a.off_bnum + (long long)sym_of(pkA, k) * N + j], gk[k]);
                             }
                         }
                     }
-                    f_hi = fs[0];
-                    if constexpr (LR) fu_hi = fus[0];
+                    if constexpr (!PT) {
+                        f_hi = fs[0];
+                        if constexpr (LR) fu_hi = fus[0];
+                    }
                 };
-                for (int c = cl; c >= 0; --c) {
-                    const int cn = c >= 2 ? c - 2 : 0;  // global prefetch two chunks ahead
-                    const double ckC = ldck(cn);
-                    const uint4 spC = ldsp(cn), pkC = loadpack(cn);
-                    if (RAG || c == cl) chunk(c, std::true_type{});
-                    else chunk(c, std::false_type{});
-                    ckA = ckB; spA = spB; pkA = pkB;
-                    ckB = ckC; spB = spC; pkB = pkC;
+                auto body = [&](int c, auto R_, auto MASK_) {
+                    constexpr int r = decltype(R_)::value;
+                    constexpr int rn = (r + 1) & 3;
+                    CHUNKSTAMP(1, c);
+                    chunk(c, X[r], X[rn].pk, E[r & 1], BU[r & 1], E[(r + 1) & 1], BU[(r + 1) & 1], MASK_);
+                    if (c >= 4) X[r] = ldset(c - 4);
+                };
+                using Mk = std::integral_constant<bool, RAG>;  // only the first chunk is masked in full waves
+                body(cl, std::integral_constant<int, 0>{}, std::true_type{});  // holds t = Tw - 1
+                for (int c = cl - 1; c >= 0; c -= 4) {
+                    body(c, std::integral_constant<int, 1>{}, Mk{});
+                    if (c >= 1) body(c - 1, std::integral_constant<int, 2>{}, Mk{});
+                    if (c >= 2) body(c - 2, std::integral_constant<int, 3>{}, Mk{});
+                    if (c >= 3) body(c - 3, std::integral_constant<int, 0>{}, Mk{});
                 }
             };
             if (safe) {
@@ -622,11 +715,14 @@ __global__ void __launch_bounds__(kBlock) k_estep_small(EArgs a) {
             }
             gall += gex;
             PHASE(3);
-            // xi_t(i,j) = a_ij * (the accumulated S_ij): scale once per sequence group
+            // xi_t(i,j) = a_ij * (the accumulated S_ij): scale once per sequence group (PT already
+            // accumulates xi itself)
+            if constexpr (!PT) {
 #pragma unroll
-            for (int k = 0; k < NS; ++k) {
-                if constexpr (LR) S[k] *= (k == 0 ? a_dg : a_up);
-                else S[k] *= arow[k];
+                for (int k = 0; k < NS; ++k) {
+                    if constexpr (LR) S[k] *= (k == 0 ? a_dg : a_up);
+                    else S[k] *= arow[k];
+                }
             }
         }
     }
@@ -1134,8 +1230,8 @@ __device__ __forceinline__ double wave_max(double x) {
     return fmax(x, __shfl_xor(x, 32));
 }
 
-template <int N, int G, int GP, bool HIST>
-__device__ bool merged_mstep(const EArgs &a, double *sBt, double *sBn, double *sPA) {
+template <int N, int G, int GP, bool HIST, bool PT>
+__device__ bool merged_mstep(const EArgs &a, double *sBt, double2 *sBP, double *sBn, double *sPA) {
     constexpr int NSM = N + N * N + 2 * N;  // pi_num, xi, gamma_den_excl, gamma_den_all
     constexpr int NW = kBlock / 64;
     constexpr int SB = kMergedMaxStats / kBlock;
@@ -1238,6 +1334,17 @@ __device__ bool merged_mstep(const EArgs &a, double *sBt, double *sBn, double *s
     constexpr bool kSameState = (kBlock % N) == 0;
     const int jj0 = ((e0 % N) + N) % N;
     const double inv0 = kSameState ? mstep_inv(sSm[N + N * N + N + jj0]) : 0.0;
+    // PT: a_jj and a_{j-1,j} of the element's state, the same arithmetic as sPA's A (:429-455)
+    auto a_of = [&](int r, int c) -> double {
+        const double den = sSm[N + N * N + r];
+        const double num = sSm[N + r * N + c];
+        return (den > 0.0 && num > 0.0) ? num / den : 0.0;
+    };
+    double ad0 = 0.0, ai0 = 0.0;
+    if constexpr (PT && kSameState) {
+        ad0 = a_of(jj0, jj0);
+        ai0 = jj0 >= 1 ? a_of(jj0 - 1, jj0) : 0.0;
+    }
     double bval[SB];
 #pragma unroll
     for (int q = 0; q < SB; ++q) {
@@ -1245,7 +1352,14 @@ __device__ bool merged_mstep(const EArgs &a, double *sBt, double *sBn, double *s
         const int jj = kSameState ? jj0 : ((e % N) + N) % N;
         const double inv = kSameState ? inv0 : mstep_inv(sSm[N + N * N + N + jj]);
         bval[q] = bnum_to_b(v[q], inv);
-        if (e >= 0 && e < K * N) sBt[(e / N) * GP + jj] = bval[q];
+        if (e >= 0 && e < K * N) {
+            sBt[(e / N) * GP + jj] = bval[q];
+            if constexpr (PT) {
+                const double ad = kSameState ? ad0 : a_of(jj, jj);
+                const double ai = kSameState ? ai0 : (jj >= 1 ? a_of(jj - 1, jj) : 0.0);
+                sBP[(e / N) * GP + jj] = double2{ad * bval[q], ai * bval[q]};
+            }
+        }
     }
     if (w0) {
 #pragma unroll
@@ -1262,8 +1376,12 @@ __device__ bool merged_mstep(const EArgs &a, double *sBt, double *sBn, double *s
     for (int i = tid; i < (K + 1) * (GP - N); i += kBlock) {
         const int k = i / (GP - N), c = N + (i - k * (GP - N));
         sBt[k * GP + c] = 0.0;
+        if constexpr (PT) sBP[k * GP + c] = double2{0.0, 0.0};
     }
-    if (tid < N) sBt[K * GP + tid] = 0.0;
+    if (tid < N) {
+        sBt[K * GP + tid] = 0.0;
+        if constexpr (PT) sBP[K * GP + tid] = double2{0.0, 0.0};
+    }
     if constexpr (HIST) {
         double2 *z2 = reinterpret_cast<double2 *>(sBn);
         for (int i = tid; i < K * GP / 2; i += kBlock) z2[i] = double2{0.0, 0.0};
@@ -1607,7 +1725,8 @@ int launch_estep(hmmbw_ctx *c, bool fwd_only, const IterState *state, double *co
         if (!f) return fail(HMMBW_E_UNSUPPORTED, "no kernel for N");
         const int NV = (lr ? 2 : c->N) + 3;
         const size_t GP = (size_t)c->G + 1;
-        const size_t tabs = lds_tab ? ((size_t)c->K + 1) * GP + (fwd_only ? 0 : (size_t)c->K * GP) : 0;
+        const size_t ntab = ((((size_t)c->K + 1) * GP) + 1) & ~(size_t)1;
+        const size_t tabs = lds_tab ? ntab * (lr ? 3 : 1) + (fwd_only ? 0 : (size_t)c->K * GP) : 0;
         size_t lds = sizeof(double) * (tabs + (size_t)wpb * c->G * NV + 8);
         if (int rc = launch_lds(f, grid, lds, c->stream, a)) return rc;
     }
@@ -1817,7 +1936,7 @@ int hmmbw_set_observations(hmmbw_ctx *c, const int64_t *offsets, const int32_t *
     // packs hold LDS byte offsets of the emission rows when the tables live in LDS (< 48 KiB, so
     // they fit uint16), symbol ids otherwise
     const bool lds_off = c->lds_tables();
-    const long long row_bytes = (long long)(c->G + 1) * (long long)sizeof(double);
+    const long long row_bytes = (long long)(c->G + 1) * 2 * (long long)sizeof(double);  // 16-B entries
     std::vector<uint16_t> hsym((size_t)std::max(symtot, 1LL), 0);
     for (long long w = 0; w < nwaves; ++w)
         for (int u = 0; u < U; ++u) {
@@ -2090,6 +2209,13 @@ int hmmbw_debug_phase_times(unsigned long long *out, int64_t nwaves) {
     if (!out || nwaves < 0 || nwaves > kPhaseWaves) return fail(HMMBW_E_INVALID, "bad argument");
     HIP_TRY(hipDeviceSynchronize());
     HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase), sizeof(unsigned long long) * 8 * nwaves));
+    return HMMBW_OK;
+}
+
+int hmmbw_debug_chunk_times(unsigned long long *out, int64_t nwaves) {
+    if (!out || nwaves < 0 || nwaves > 4096) return fail(HMMBW_E_INVALID, "bad argument");
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_chunk), sizeof(unsigned long long) * 128 * nwaves));
     return HMMBW_OK;
 }
 #endif

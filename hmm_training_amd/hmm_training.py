@@ -192,7 +192,7 @@ def hmm_training(observations: List[np.ndarray], N: int = 4, M: int = 256, epsil
 
 
 def training_with_save(word_recordings, centroids, word_name: str, max_iterations=100, show_progress=True,
-                       load_initial_params=False, *, n_states: int = 4) -> HMMTrained:
+                       load_initial_params=False, *, n_states: int = 4, base_dir: Optional[str] = None) -> HMMTrained:
     """VQ -> hmm_training(N=4) -> HMMTrained -> save JSON (hmm_training.py:215-247)."""
     print("Converting recordings to observations...")
     observations = get_observations(word_recordings, centroids)
@@ -203,5 +203,8 @@ def training_with_save(word_recordings, centroids, word_name: str, max_iteration
                             show_progress=show_progress, word_name=word_name,
                             load_initial_params=load_initial_params)
     model = HMMTrained(states=n_states, symbols=len(centroids), A=A, B=B, Pi=pi, word=word_name)
-    DataStorageHMM.save_hmm(model, print_messages=False)
+    if base_dir is None:
+        DataStorageHMM.save_hmm(model, print_messages=False)
+    else:
+        DataStorageHMM.save_hmm(model, base_dir=base_dir, print_messages=False)
     return model

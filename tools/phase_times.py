@@ -74,6 +74,20 @@ def main():
             r = us(t[:, k] - t0)
             print(f"at {nm:<12s} rel-start  min {r.min():7.2f}  p50 {np.median(r):7.2f}  max {r.max():7.2f} us")
     np.save(os.path.join(out_dir, "phase_nomerge.npy" if a.no_merge else "phase_merge.npy"), t)
+    # per-chunk shader-clock durations (forward: chunk c -> c+1; backward: chunk c -> c-1)
+    ck = np.zeros((nw_pad, 2, 64), dtype=np.uint64)
+    l.hmmbw_debug_chunk_times.argtypes = [ctypes.c_void_p, ctypes.c_int64]
+    assert l.hmmbw_debug_chunk_times(ck.ctypes.data, nw_pad) == 0
+    ck = ck[:nw].astype(np.int64)
+    nch = (T + 7) // 8
+    fwd = np.diff(ck[:, 0, :nch], axis=1)
+    bwd = -np.diff(ck[:, 1, :nch], axis=1)  # stamped in descending chunk order
+    span_clk = (ck[:, 0, nch - 1] - ck[:, 0, 0]).astype(float)
+    span_us = us((t[:, 2] - t[:, 1]).astype(float))
+    print(f"forward chunk cycles: p50 {np.median(fwd):.0f}  mean {fwd.mean():.0f}  max {fwd.max():.0f}; per chunk p50 over waves: "
+          + " ".join(f"{np.median(fwd[:, c]):.0f}" for c in range(min(fwd.shape[1], 12))))
+    print(f"backward chunk cycles: p50 {np.median(bwd):.0f}  mean {bwd.mean():.0f}  max {bwd.max():.0f}")
+    print(f"shader clock estimate: {np.median(span_clk / np.maximum(span_us * (nch - 1) / nch, 1e-9)) / 1e3:.2f} GHz")
 
 
 if __name__ == "__main__":
