@@ -29,951 +29,10 @@
 //   k_mstep / k_mstep_staged  one workgroup: L, M-step, convergence record, zero the statistics
 //                   (staged: all statistics gathered into LDS with one batch of loads).
 //   k_finalise  the reference's return-path normalisation (:524-541).
-#include <hip/hip_runtime.h>
-
-#include <algorithm>
-#include <cmath>
-#include <cstdint>
-#include <cstdio>
-#include <cstring>
-#include <numeric>
-#include <string>
-#include <type_traits>
-#include <vector>
-
-#include "../../include/hmmbw.h"
+#include "hmmbw_device.hpp"
+#include "hmmbw_kernels.hpp"
 
 namespace hmmbw {
-
-// Diagnostics build only (-DHMMBW_PHASE_TIMES, tools/phase_times.py): per-wave wall-clock stamps of
-// the small E-step's phases, read back with hmmbw_debug_phase_times.
-#ifdef HMMBW_PHASE_TIMES
-constexpr int kPhaseWaves = 1 << 16;
-__device__ unsigned long long g_phase[kPhaseWaves][8];
-#define PHASE(k)                                                                               \
-    do {                                                                                       \
-        const long long w_ = (long long)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);   \
-        if ((threadIdx.x & 63) == 0 && w_ < kPhaseWaves) g_phase[w_][k] = wall_clock64();      \
-    } while (0)
-// shader-clock stamp at the start of forward (d = 0) / backward (d = 1) chunk c (c < 64)
-__device__ unsigned long long g_chunk[4096][2][64];
-#define CHUNKSTAMP(d, c)                                                                       \
-    do {                                                                                       \
-        const long long w_ = (long long)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);   \
-        if ((threadIdx.x & 63) == 0 && w_ < 4096 && (c) < 64) g_chunk[w_][d][c] = clock64();   \
-    } while (0)
-#else
-#define CHUNKSTAMP(d, c) \
-    do {                 \
-    } while (0)
-#define PHASE(k) \
-    do {         \
-    } while (0)
-#endif
-
-constexpr int kWave = 64;
-constexpr int kChunk = 8;  // time steps per packed symbol load (8 x uint16 = 16 B)
-constexpr int kScale = 4;  // lagged mode: the forward rescales every kScale steps
-constexpr int kHist = 4096;
-constexpr int kBlock = 256;  // threads per E-step workgroup (4 waves)
-
-struct IterState {
-    double prev_L;
-    double last_L;
-    double last_diff;
-    double epsilon;
-    long long iteration;
-    long long max_iterations;
-    int done;
-    int converged;
-};
-
-// Observation layout in HBM (built once by hmmbw_set_observations).
-//   slot = wave * U + u  ->  caller sequence slot_seq[slot] (-1: padding), length slot_len[slot]
-//   sym    : per wave, chunk-major [chunk][u][8] uint16  (one 16-B load = 8 steps of one sequence)
-//   ckpt   : per wave [chunk][64 lanes] fp64 — alpha_hat at the first step of every chunk (small N)
-//   spack  : per wave [chunk][u] 8 x int16 — the power-of-two scale exponent of every step
-//   alpha  : per wave [t][64 lanes] fp64 + ebuf [t][u] int32 — full alpha_hat (wide kernel only)
-struct Layout {
-    const uint16_t *sym;
-    const long long *wave_symoff;
-    const long long *wave_ckoff;   // doubles (small) | alpha doubles (wide)
-    const long long *wave_spoff;   // uint4 units (small) | ebuf ints (wide)
-    const int *wave_T;
-    const int *wave_full;          // 1: every real slot of the wave has length wave_T
-    const int *slot_len;
-    const int *slot_seq;
-    long long nwaves;
-};
-
-struct MArgs {
-    const double *src;     // statistics: the copies (single rank) or the all-reduced buffer
-    double *zero_ll;       // LL slots to clear (multi-rank) or nullptr
-    int nsrc;
-    long long copy_len;
-    double *pi, *A, *B, *Bt;
-    const double *llpart;
-    long long nblocks;
-    long long R_global;
-    const IterState *state;  // convergence state entering this M-step
-    IterState *state_out;    // ... and after it (double-buffered: the host flips the slots per M-step)
-    double *hist;
-    int N, K, G, world;
-    int local_lse;
-    long long off_S, off_gex, off_gall, off_bnum, off_ll;
-};
-
-struct EArgs {
-    Layout L;
-    const double *pi;
-    const double *A;
-    const double *Bt;  // [K][G] + G zero pad
-    double *ckpt;      // small: checkpoints | wide: alpha_hat
-    uint4 *spack;      // small: scale exponents
-    int *ebuf;         // wide: scale exponents
-    double *copies;    // [ncopies][copy_len] statistics accumulators (workgroup b adds into copy b % ncopies)
-    long long copy_len;
-    int ncopies;
-    double *logp;
-    double *llpart;    // [blocks][2]: per-block (max, sum exp) of log P
-    const IterState *state;
-    int K;
-    int N;
-    int force_safe;    // 1: per-step normalisation (no lagged scaling)
-    int ablate;        // diagnostics only: bit 0 skips the statistics flush, bit 1 the backward sweep
-    int merged;        // 1: run the previous iteration's M-step (m) in the prologue of every workgroup
-    double *zero;      // statistics buffer of the NEXT iteration, cleared by this launch (or nullptr)
-    long long zero_len;
-    MArgs m;
-    long long off_S, off_gex, off_gall, off_bnum;
-};
-
-// ---------------------------------------------------------------------------------------------
-// Cross-lane helpers (DPP on gfx950; 64-bit operands are split or use v_mov_b64_dpp)
-// ---------------------------------------------------------------------------------------------
-template <int CTRL>
-__device__ __forceinline__ double dpp(double v) {
-    long long x = __builtin_bit_cast(long long, v);
-    x = __builtin_amdgcn_update_dpp(0ll, x, CTRL, 0xF, 0xF, true);
-    return __builtin_bit_cast(double, x);
-}
-
-template <int CTRL>
-__device__ __forceinline__ int dpp_i32(int v) {
-    return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, true);
-}
-
-// Sum over a group of G lanes (butterfly; every lane gets the bitwise-identical result because
-// each level adds the same two partial sums, only commuted).
-template <int G>
-__device__ __forceinline__ double gsum(double x) {
-    if constexpr (G >= 2) x += dpp<0xB1>(x);   // quad_perm [1,0,3,2]
-    if constexpr (G >= 4) x += dpp<0x4E>(x);   // quad_perm [2,3,0,1]
-    if constexpr (G >= 8) x += dpp<0x141>(x);  // row_half_mirror
-    if constexpr (G >= 16) x += dpp<0x140>(x); // row_mirror
-    if constexpr (G >= 32) x += __shfl_xor(x, 16);
-    if constexpr (G >= 64) x += __shfl_xor(x, 32);
-    return x;
-}
-
-template <int G>
-__device__ __forceinline__ int gmax_i32(int e) {
-    if constexpr (G >= 2) e = max(e, dpp_i32<0xB1>(e));
-    if constexpr (G >= 4) e = max(e, dpp_i32<0x4E>(e));
-    if constexpr (G >= 8) e = max(e, dpp_i32<0x141>(e));
-    if constexpr (G >= 16) e = max(e, dpp_i32<0x140>(e));
-    return e;
-}
-
-// Exponent that steers the power-of-two scaling: frexp exponent of the group's largest entry
-// (entries are >= 0), kZeroExp when the whole group is zero.
-constexpr int kZeroExp = -8192;
-template <int G>
-__device__ __forceinline__ int group_exp(double z) {
-    return gmax_i32<G>(z > 0.0 ? __builtin_amdgcn_frexp_exp(z) : kZeroExp);
-}
-
-// Value of lane I of this lane's G-group.
-template <int G, int I>
-__device__ __forceinline__ double gbcast(double v, int lane) {
-    if constexpr (G == 2) {
-        return dpp<(I) | ((I) << 2) | ((2 + I) << 4) | ((2 + I) << 6)>(v);
-    } else if constexpr (G == 4) {
-        return dpp<(I) * 0x55>(v);
-    } else if constexpr (G == 8) {
-        const double lo = dpp<0x150 + I>(v);
-        const double hi = dpp<0x150 + 8 + I>(v);
-        return (lane & 8) ? hi : lo;
-    } else {
-        static_assert(G == 16, "group size");
-        return dpp<0x150 + I>(v);  // row_newbcast:I
-    }
-}
-
-template <int B, int E, class F>
-__device__ __forceinline__ void sfor(F &&f) {
-    if constexpr (B < E) {
-        f(std::integral_constant<int, B>{});
-        sfor<B + 1, E>(f);
-    }
-}
-
-__device__ __forceinline__ int sym_of(const uint4 &p, int s) {
-    const unsigned w = s < 2 ? p.x : (s < 4 ? p.y : (s < 6 ? p.z : p.w));
-    return (s & 1) ? int(w >> 16) : int(w & 0xFFFFu);
-}
-
-__device__ __forceinline__ int exp_of(const uint4 &p, int s) {  // signed int16 lanes of a pack
-    const unsigned w = s < 2 ? p.x : (s < 4 ? p.y : (s < 6 ? p.z : p.w));
-    return (s & 1) ? int((int)w >> 16) : int((int)(w << 16) >> 16);
-}
-
-__device__ __forceinline__ uint4 pack_exps(const int *e) {
-    uint4 p;
-    p.x = (unsigned)(e[0] & 0xFFFF) | ((unsigned)e[1] << 16);
-    p.y = (unsigned)(e[2] & 0xFFFF) | ((unsigned)e[3] << 16);
-    p.z = (unsigned)(e[4] & 0xFFFF) | ((unsigned)e[5] << 16);
-    p.w = (unsigned)(e[6] & 0xFFFF) | ((unsigned)e[7] << 16);
-    return p;
-}
-
-__device__ __forceinline__ double pow2_scale(double x, int e) { return __builtin_amdgcn_ldexp(x, -e); }
-
-// Per-block (max, sum exp(x - max)) of the sequences' log P (each sequence contributes from
-// exactly one lane with valid = true).  All threads of the block call it.
-__device__ void block_ll_partial(double lp, bool valid, double *sh, double *out) {
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, nw = blockDim.x >> 6;
-    double m = valid ? lp : -INFINITY;
-    for (int k = 32; k >= 1; k >>= 1) m = fmax(m, __shfl_xor(m, k));
-    if (lane == 0) sh[wv] = m;
-    __syncthreads();
-    double M = -INFINITY;
-    for (int w = 0; w < nw; ++w) M = fmax(M, sh[w]);
-    double s = (valid && M != -INFINITY && lp != -INFINITY) ? exp(lp - M) : 0.0;
-    for (int k = 32; k >= 1; k >>= 1) s += __shfl_xor(s, k);
-    __syncthreads();
-    if (lane == 0) sh[wv] = s;
-    __syncthreads();
-    if (tid == 0) {
-        double S = 0.0;
-        for (int w = 0; w < nw; ++w) S += sh[w];
-        // memory-side atomics: the fused M-step of the last workgroup reads these with atomics too
-        atomicExch(&out[0], (S > 0.0) ? M : 0.0);
-        atomicExch(&out[1], S);
-    }
-}
-
-// ---------------------------------------------------------------------------------------------
-// Small-N E-step / scorer.  One G-lane group per sequence (lane j = state j), 64/G per wave.
-//
-// Forward: z_t = alpha_t / 2^{C_t}, C_t = s_0 + ... + s_t.  In the default (lagged) mode only every
-// kScale-th step rescales, by s_t = M_{t-kScale} - 1023 with M = the biased exponent of the group's
-// largest entry measured kScale steps earlier, so the per-step dependency chain is just
-// (DPP shift || multiply) -> fma; the scaling itself is folded into the emission factor
-// b_j(o_t) * 2^{-s_t} (exact).  If a wave's magnitudes ever leave [2^-900, 2^900]
-// (pathological parameters) the wave re-runs its forward in the safe mode, which normalises every
-// step by its own group maximum.  Only z at the first step of every 8-step chunk (the checkpoint)
-// and the s_t are stored; the backward sweep recomputes each chunk's z_t in registers with the
-// identical instruction sequence (bit-identical), so alpha never round-trips through HBM.
-//
-// Backward (Rabiner scaling with c_t = 2^{s_t}): beta_hat_{T-1} = 1/phat, phat = sum_j z_{T-1}(j);
-//   v_j = b_j(o_{t+1}) 2^{-s_{t+1}} beta_hat_{t+1}(j),  beta_hat_t(i) = sum_j a_ij v_j,
-//   gamma_t(i) = z_t(i) beta_hat_t(i),  xi_t(i,j) = a_ij z_t(i) v_j  (accumulated as S_ij = xi/a_ij).
-// gamma is scattered into the per-workgroup LDS histogram B_num[o_t][j] (ds_add_f64).
-// ---------------------------------------------------------------------------------------------
-template <int N, int G, int GP, bool HIST, bool PT>
-__device__ bool merged_mstep(const EArgs &a, double *sBt, double2 *sBP, double *sBn, double *sPA);
-
-template <int N, int G, bool LR, bool LDSTAB, bool FWD_ONLY>
-__global__ void __launch_bounds__(kBlock) k_estep_small(EArgs a) {
-    constexpr int U = kWave / G;
-    constexpr int NS = LR ? 2 : N;      // per-lane S accumulators (row j of S)
-    constexpr int NV = NS + 3;          // + gamma_den_excl, gamma_den_all, pi_num
-    constexpr int GP = LDSTAB ? G + 1 : G;  // row stride of the emission / histogram tables
-    // left-to-right with LDS tables: per (symbol, state) products {a_jj b_j(o), a_{j-1,j} b_j(o)}
-    constexpr bool PT = LR && LDSTAB;
-    extern __shared__ double smem[];
-    __shared__ double sPA[G + N * N];  // pi (zero-padded to G) and A of this iteration
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    PHASE(0);
-    if constexpr (!FWD_ONLY)  // clear the next iteration's statistics (single rank: triple buffer)
-        for (long long i = (long long)blockIdx.x * blockDim.x + tid; i < a.zero_len;
-             i += (long long)gridDim.x * blockDim.x)
-            a.zero[i] = 0.0;
-    const int j = lane & (G - 1), u = lane / G;
-    const int K = a.K;
-    const size_t ntab = LDSTAB ? (((size_t)K + 1) * GP + 1) & ~(size_t)1 : 0;  // even: 16-B alignment
-    double *sBt = smem;                                               // [K+1][GP] b_j(o)
-    double2 *sBP = reinterpret_cast<double2 *>(smem + ntab);          // PT: [K+1][GP] products
-    double *sBn = smem + ntab + (PT ? 2 * ntab : 0);                  // [K][GP] B numerator histogram
-    double *sRed = sBn + ((LDSTAB && !FWD_ONLY) ? (size_t)K * GP : 0); // [waves][G][NV] + ll scratch
-    bool merged = false;
-    if constexpr (LDSTAB && !FWD_ONLY) merged = a.merged != 0;
-    if (merged) {
-        // the previous iteration's M-step, computed redundantly by every workgroup straight into
-        // its LDS tables (no separate M-step kernel, no parameter round trip through HBM)
-        if constexpr (LDSTAB && !FWD_ONLY)
-            if (!merged_mstep<N, G, GP, true, PT>(a, sBt, sBP, sBn, sPA)) return;  // done or stopped (:346)
-    } else {
-        if (a.state != nullptr && a.state->done) return;  // converged: device-side no-op
-        if (tid < G) sPA[tid] = tid < N ? a.pi[tid] : 0.0;
-        if (tid < N * N) sPA[G + tid] = a.A[tid];
-        if constexpr (LDSTAB) {
-            // 16 independent loads in flight per thread before the first LDS store
-            constexpr int TB = 16;
-            const int nt = (K + 1) * GP;
-            for (int i0 = 0; i0 < nt; i0 += TB * kBlock) {
-                double x[TB];
-#pragma unroll
-                for (int q = 0; q < TB; ++q) {
-                    const int i = i0 + q * kBlock + tid;
-                    const int k = i / GP, c = i - k * GP;
-                    const bool ok = i < nt && k < K && c < G;
-                    x[q] = a.Bt[ok ? (size_t)k * G + c : 0];
-                    x[q] = ok ? x[q] : 0.0;
-                }
-#pragma unroll
-                for (int q = 0; q < TB; ++q) {
-                    const int i = i0 + q * kBlock + tid;
-                    if (i < nt) {
-                        sBt[i] = x[q];
-                        if constexpr (!FWD_ONLY)
-                            if (i < K * GP) sBn[i] = 0.0;
-                    }
-                }
-            }
-        }
-        __syncthreads();
-        if constexpr (PT) {
-            for (int i = tid; i < (K + 1) * GP; i += kBlock) {
-                const int c = i % GP;
-                const double b = sBt[i];
-                const double ad = c < N ? sPA[G + c * N + c] : 0.0;
-                const double ai = (c >= 1 && c < N) ? sPA[G + (c - 1) * N + c] : 0.0;
-                sBP[i] = double2{ad * b, ai * b};
-            }
-            __syncthreads();
-        }
-    }
-    const double *Btab = LDSTAB ? sBt : a.Bt;
-    PHASE(1);
-
-    const long long wave = (long long)blockIdx.x * (blockDim.x >> 6) + wv;
-    double *accb = a.copies + (long long)(blockIdx.x % a.ncopies) * a.copy_len;
-    double S[NS];
-#pragma unroll
-    for (int k = 0; k < NS; ++k) S[k] = 0.0;
-    double gex = 0.0, gall = 0.0, pin = 0.0;
-    double logp_lane = -INFINITY;
-    bool ll_valid = false;
-
-    if (wave < a.L.nwaves) {
-        const long long slot = wave * U + u;
-        const int T = a.L.slot_len[slot];
-        const int seq = a.L.slot_seq[slot];
-        const int Tw = a.L.wave_T[wave];
-        const bool full = a.L.wave_full[wave] != 0;
-        const int nch = (Tw + kChunk - 1) / kChunk;
-        const uint16_t *symw = a.L.sym + a.L.wave_symoff[wave] + u * kChunk;
-        double *ckw = a.ckpt + (FWD_ONLY ? 0 : a.L.wave_ckoff[wave]) + lane;
-        uint4 *spw = a.spack + (FWD_ONLY ? 0 : a.L.wave_spoff[wave]) + u;
-        const bool jv = j < N;
-
-        // transition coefficients of this lane (state j)
-        double acol[LR ? 1 : N], arow[LR ? 1 : N];
-        double a_dg = 0.0, a_in = 0.0, a_up = 0.0;
-        const double *sA = sPA + G;
-        if constexpr (LR) {
-            a_dg = jv ? sA[j * N + j] : 0.0;
-            a_in = (jv && j >= 1) ? sA[(j - 1) * N + j] : 0.0;
-            a_up = (j + 1 < N) ? sA[j * N + j + 1] : 0.0;
-        } else {
-#pragma unroll
-            for (int i = 0; i < N; ++i) {
-                acol[i] = jv ? sA[i * N + j] : 0.0;
-                arow[i] = jv ? sA[j * N + i] : 0.0;
-            }
-        }
-        const double pij = sPA[j];
-
-        auto loadpack = [&](int c) -> uint4 {
-            return *reinterpret_cast<const uint4 *>(symw + (long long)c * U * kChunk);
-        };
-        // Emission-table element of this lane for packed entry k.  With LDS tables the packs hold the
-        // byte offset of the symbol's row in the 16-byte product table (o * GP * 16, precomputed on
-        // the host; half of it in the 8-byte tables), else the symbol.
-        const char *tabj = reinterpret_cast<const char *>(Btab + j);
-        auto brow = [&](const uint4 &p, int k) -> const double * {
-            if constexpr (LDSTAB) return reinterpret_cast<const double *>(tabj + (sym_of(p, k) >> 1));
-            else return reinterpret_cast<const double *>(tabj) + (size_t)sym_of(p, k) * GP;
-        };
-        // the emission operand of one step: the product pair (PT) or b_j(o)
-        using Em = typename std::conditional<PT, double2, double>::type;
-        const char *tabPj = reinterpret_cast<const char *>(sBP + j);
-        auto ld_em = [&](const uint4 &p, int k) -> Em {
-            if constexpr (PT) return *reinterpret_cast<const double2 *>(tabPj + sym_of(p, k));
-            else return *brow(p, k);
-        };
-        // One forward step (hmm_training.py:122-160 without the 2^-s rescale, which the caller
-        // applies): PT  a_jj b_j z_{t-1}(j) + a_{j-1,j} b_j z_{t-1}(j-1);  LR  the same from a and b;
-        // dense  (A^T z_{t-1})_j b_j.  Used verbatim by the forward sweep and the backward recompute,
-        // so both produce bit-identical z_t.
-        auto step = [&](double zp, Em e) -> double {
-            if constexpr (PT) {
-                const double prev = dpp<0x111>(zp);  // row_shr:1 -> z_{t-1}(j-1); 0 in lane 0 of a group
-                return fma(e.y, prev, e.x * zp);
-            } else if constexpr (LR) {
-                const double prev = dpp<0x111>(zp);  // row_shr:1 -> z_{t-1}(j-1); a_in = 0 for j = 0
-                return fma(a_in * e, prev, (a_dg * e) * zp);
-            } else {
-                const double bs = e;
-                double acc0 = 0.0, acc1 = 0.0;
-                sfor<0, N>([&](auto I) {
-                    const double zi = gbcast<G, I.value>(zp, lane);
-                    if constexpr ((I.value & 1) == 0) acc0 = fma(acol[I.value], zi, acc0);
-                    else acc1 = fma(acol[I.value], zi, acc1);
-                });
-                return (acc0 + acc1) * bs;
-            }
-        };
-        // Biased exponent field of the group's largest entry (entries are >= 0; 0 for an all-zero
-        // group).  Integer-only: bit-field extract + DPP max.
-        auto group_bexp = [&](double x) -> int {
-            return gmax_i32<G>((int)__builtin_amdgcn_ubfe((unsigned)__double2hiint(x), 20, 11));
-        };
-
-        // ---------------- forward sweep (hmm_training.py:357-368) ----------------
-        // Lagged mode: only steps t = 0 mod kScale rescale; s_t = M_{t-kScale}, the group exponent
-        // measured right after step t-kScale, so C_t = log2|alpha_{t-kScale}| and the stored z stay
-        // within a few steps' growth of 1.
-        double z = 0.0;
-        int C = 0;
-        auto forward = [&](auto SAFE_, auto RAG_) -> bool {
-            constexpr bool SAFE = decltype(SAFE_)::value;
-            constexpr bool RAG = decltype(RAG_)::value;
-            z = 0.0;
-            C = 0;
-            int pend[kChunk / kScale] = {};  // lagged: exponents to apply at the coming scale steps
-            int minM = 4096, maxM = 0;       // extreme group exponents seen (fallback trigger)
-            // Symbol packs travel through a 4-deep register ring (the pack of chunk c + 4 is loaded
-            // while chunk c runs) and the emissions through a 2-deep one (chunk c + 1's LDS reads are
-            // issued before chunk c computes); the sweep is unrolled by 4 so no ring slot is ever
-            // copied, which would wait on the load that just filled it.
-            uint4 Q[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) Q[i] = loadpack(i < nch ? i : nch - 1);
-            const double b00 = *brow(Q[0], 0);  // b_j(o_0) for pi_j b_j(o_0) (:357-360)
-            Em E[2][kChunk];
-#pragma unroll
-            for (int k = 0; k < kChunk; ++k) E[0][k] = ld_em(Q[0], k);
-            auto chunk = [&](int c, const Em (&bv)[kChunk], auto MASK_) {
-                constexpr bool MASK = decltype(MASK_)::value;
-                const int Tend = RAG ? T : Tw;
-                int sp[kChunk];
-#pragma unroll
-                for (int k = 0; k < kChunk; ++k) {
-                    const int t = c * kChunk + k;
-                    double zn;
-                    int st = 0;
-                    if constexpr (SAFE) {
-                        const double x = (t == 0) ? pij * b00 : step(z, bv[k]);
-                        const int M = group_bexp(x);
-                        st = M == 0 ? 0 : M - 1023;
-                        zn = pow2_scale(x, st);
-                    } else if (k % kScale == 0) {
-                        st = pend[k / kScale];
-                        zn = pow2_scale((t == 0) ? pij * b00 : step(z, bv[k]), st);
-                        const int M = group_bexp(zn);
-                        // applied kScale steps later; clamped so an all-zero (dead) group can never
-                        // scale itself to inf (the fallback below catches it)
-                        pend[k / kScale] = min(max(M - 1023, -600), 600);
-                        if (!RAG || t < T) {
-                            minM = min(minM, M);
-                            maxM = max(maxM, M);
-                        }
-                    } else {
-                        zn = step(z, bv[k]);
-                    }
-                    if constexpr (MASK) {
-                        const bool act = t < Tend;
-                        z = act ? zn : z;
-                        C += act ? st : 0;
-                    } else {
-                        z = zn;
-                        C += st;
-                    }
-                    sp[k] = st;
-                    if constexpr (!FWD_ONLY)
-                        if (k == 0) ckw[(long long)c * kWave] = z;  // checkpoint z_{8c}
-                }
-                if constexpr (!FWD_ONLY) spw[(long long)c * U] = pack_exps(sp);
-            };
-            auto body = [&](int c, auto R_) {
-                constexpr int r = decltype(R_)::value;
-                CHUNKSTAMP(0, c);
-#pragma unroll
-                for (int k = 0; k < kChunk; ++k) E[(r + 1) & 1][k] = ld_em(Q[(r + 1) & 3], k);
-                if (c + 4 < nch) Q[r] = loadpack(c + 4);
-                if (RAG || (c == nch - 1 && (Tw % kChunk) != 0)) chunk(c, E[r & 1], std::true_type{});
-                else chunk(c, E[r & 1], std::false_type{});
-            };
-            for (int c = 0; c < nch; c += 4) {
-                body(c, std::integral_constant<int, 0>{});
-                if (c + 1 < nch) body(c + 1, std::integral_constant<int, 1>{});
-                if (c + 2 < nch) body(c + 2, std::integral_constant<int, 2>{});
-                if (c + 3 < nch) body(c + 3, std::integral_constant<int, 3>{});
-            }
-            return (!SAFE) && (minM < 1023 - 900 || maxM > 1023 + 900);
-        };
-        bool safe = a.force_safe != 0;
-        if (!safe) {
-            const bool bad = full ? forward(std::false_type{}, std::false_type{})
-                                  : forward(std::false_type{}, std::true_type{});
-            safe = __any(bad && T > 0) != 0;  // wave-uniform: redo the wave with per-step normalisation
-        }
-        if (safe) {
-            if (full) forward(std::true_type{}, std::false_type{});
-            else forward(std::true_type{}, std::true_type{});
-        }
-
-        PHASE(2);
-        // log P(O|lambda) = log(sum_j z_{T-1}(j)) + ln2 * C   (:375-377)
-        const double phat = gsum<G>(z);
-        const bool alive = (T > 0) && (phat > 0.0);
-        const double lp = alive ? (log(phat) + (double)C * 0.69314718055994530942) : -INFINITY;
-        if (T > 0 && j == 0 && seq >= 0) a.logp[seq] = lp;
-        logp_lane = lp;
-        ll_valid = (T > 0) && (j == 0);
-
-        if constexpr (!FWD_ONLY) if (!(a.ablate & 2)) {
-            // ------------- backward sweep fused with gamma / xi / M-step numerators -------------
-            const double inv_p = alive ? 1.0 / phat : 0.0;  // beta_hat_{T-1}: folds 1/P (:392,:407)
-            auto backward = [&](auto SAFE_, auto RAG_) {
-                constexpr bool SAFE = decltype(SAFE_)::value;
-                constexpr bool RAG = decltype(RAG_)::value;
-                double beta = inv_p;
-                const int cl = (Tw - 1) / kChunk;
-                // per-chunk inputs (checkpoint, scale exponents, symbol pack) through a 4-deep register
-                // ring: chunk c - 4's are loaded as soon as chunk c is done with its slot; emissions
-                // through a 2-deep one; unrolled by 4 so no slot is copied (see the forward)
-                struct Ld {
-                    double ck;
-                    uint4 sp, pk;
-                };
-                auto ldset = [&](int c) -> Ld {
-                    return Ld{ckw[(long long)c * kWave], spw[(long long)c * U], loadpack(c)};
-                };
-                Ld X[4];
-#pragma unroll
-                for (int i = 0; i < 4; ++i) X[i] = ldset(cl - i >= 0 ? cl - i : 0);
-                Em E[2][kChunk];
-                double BU[2][kChunk];
-                auto ldrows = [&](Em (&bv)[kChunk], double (&bu)[kChunk], const uint4 &p) {
-#pragma unroll
-                    for (int k = 0; k < kChunk; ++k) {
-                        if constexpr (PT) {
-                            bv[k] = ld_em(p, k);
-                        } else {
-                            const double *r = brow(p, k);
-                            bv[k] = r[0];
-                            if constexpr (LR) bu[k] = r[1];  // b_{j+1}(o): the neighbour's emission
-                        }
-                    }
-                };
-                ldrows(E[0], BU[0], X[0].pk);
-                double f_hi = 0.0, fu_hi = 0.0;  // scaled emissions at o_{8c+8} (from chunk c+1)
-                Em e_hi{};                       // PT: product pair at o_{8c+8} ...
-                int s_hi = 0;                    // ... and that step's scale exponent
-                auto chunk = [&](int c, const Ld &cur, const uint4 &pkn, const Em (&bv)[kChunk],
-                                 const double (&bu)[kChunk], Em (&bvn)[kChunk], double (&bun)[kChunk],
-                                 auto MASK_) {
-                    constexpr bool MASK = decltype(MASK_)::value;
-                    const uint4 &spA = cur.sp, &pkA = cur.pk;
-                    int sk[kChunk];
-                    double fs[kChunk], fus[kChunk];  // non-PT: b(o_t) / c_t for t = 8c .. 8c+7
-#pragma unroll
-                    for (int k = 0; k < kChunk; ++k) {
-                        const bool scaled = SAFE || (k % kScale == 0);
-                        sk[k] = scaled ? exp_of(spA, k) : 0;
-                        if constexpr (!PT) {
-                            fs[k] = scaled ? pow2_scale(bv[k], sk[k]) : bv[k];
-                            if constexpr (LR) fus[k] = scaled ? pow2_scale(bu[k], sk[k]) : bu[k];
-                        }
-                    }
-                    // recompute z_{8c .. 8c+7} from the checkpoint (identical ops to the forward)
-                    double zr[kChunk];
-                    zr[0] = cur.ck;
-#pragma unroll
-                    for (int k = 1; k < kChunk; ++k) {
-                        const double x = step(zr[k - 1], bv[k]);
-                        zr[k] = (SAFE || (k % kScale == 0)) ? pow2_scale(x, sk[k]) : x;
-                    }
-                    double gk[kChunk];
-#pragma unroll
-                    for (int k = kChunk - 1; k >= 0; --k) {
-                        const int t = c * kChunk + k;
-                        const double zt = zr[k];
-                        // regular step (t <= T-2) / gamma_{T-1} (t == T-1) / past the end; per lane in
-                        // ragged waves, wave-uniform otherwise; only boundary chunks are masked.
-                        // zs = 0 leaves S and gex unchanged.
-                        const bool reg = !MASK || (RAG ? (t <= T - 2) : (t <= Tw - 2));
-                        const bool ini = MASK && (RAG ? (t == T - 1) : (t == Tw - 1));
-                        const double zs = reg ? zt : 0.0;
-                        double bn;
-                        if constexpr (PT) {
-                            // beta_hat_t(j) = a_jj b_j(o') beta'(j) + a_j,j+1 b_j+1(o') beta'(j+1) with
-                            // beta' = beta_hat_{t+1} / c_{t+1} (:163-199); the second term is the
-                            // neighbour's a_{j,j+1} b_{j+1} beta' product, shifted down one lane (zero
-                            // past the last state: a_{N-1,N} does not exist, Bi(., 0) = 0)
-                            const Em e = (k == kChunk - 1) ? e_hi : bv[k + 1];
-                            const int s1 = (k == kChunk - 1) ? s_hi : sk[(k + 1) & (kChunk - 1)];
-                            const bool sc1 = SAFE || ((k + 1) % kScale == 0);
-                            const double bp = sc1 ? pow2_scale(beta, s1) : beta;
-                            const double vd = e.x * bp;
-                            const double vu = dpp<0x101>(e.y * bp);  // row_shl:1
-                            bn = vd + vu;
-                            S[0] = fma(zs, vd, S[0]);  // xi_t(j,j)   (:396-410)
-                            S[1] = fma(zs, vu, S[1]);  // xi_t(j,j+1)
-                        } else if constexpr (LR) {
-                            const double f = (k == kChunk - 1) ? f_hi : fs[k + 1];  // b(o_{t+1}) / c_{t+1}
-                            const double fu = (k == kChunk - 1) ? fu_hi : fus[k + 1];
-                            const double bup = dpp<0x101>(beta);  // row_shl:1 -> beta(j+1)
-                            const double vd = f * beta, vu = fu * bup;
-                            bn = fma(a_up, vu, a_dg * vd);       // :182-197
-                            S[0] = fma(zs, vd, S[0]);             // xi_t(j,j)   / a_jj
-                            S[1] = fma(zs, vu, S[1]);             // xi_t(j,j+1) / a_j,j+1 (scaled at the end)
-                        } else {
-                            const double f = (k == kChunk - 1) ? f_hi : fs[k + 1];  // b(o_{t+1}) / c_{t+1}
-                            const double vd = f * beta;
-                            double b0 = 0.0, b1 = 0.0;
-                            sfor<0, N>([&](auto I) {
-                                const double vk = gbcast<G, I.value>(vd, lane);
-                                if constexpr ((I.value & 1) == 0) b0 = fma(arow[I.value], vk, b0);
-                                else b1 = fma(arow[I.value], vk, b1);
-                                S[I.value] = fma(zs, vk, S[I.value]);   // :402-408
-                            });
-                            bn = b0 + b1;
-                        }
-                        double g;  // gamma_t(j) (:392)
-                        if constexpr (MASK) {
-                            g = reg ? zt * bn : (ini ? zt * inv_p : 0.0);
-                            beta = reg ? bn : beta;
-                            gex = fma(zs, bn, gex);
-                            gall += ini ? g : 0.0;
-                        } else {
-                            g = zt * bn;
-                            beta = bn;
-                            gex += g;
-                        }
-                        if (t == 0) pin = g;  // :420
-                        gk[k] = g;
-                    }
-                    if constexpr (PT) {
-                        e_hi = bv[0];
-                        s_hi = sk[0];
-                    }
-                    // next chunk's emission rows go to LDS before this chunk's histogram atomics, so
-                    // they are not queued behind them
-                    ldrows(bvn, bun, pkn);
-                    if ((N == G || jv) && !(a.ablate & 4)) {
-#pragma unroll
-                        for (int k = 0; k < kChunk; ++k) {  // :474-485
-                            if constexpr (LDSTAB) {
-                                atomicAdd(reinterpret_cast<double *>(reinterpret_cast<char *>(sBn + j) + (sym_of(pkA, k) >> 1)), gk[k]);
-                            } else if (gk[k] != 0.0) {
-                                unsafeAtomicAdd(&accb[a.off_bnum + (long long)sym_of(pkA, k) * N + j], gk[k]);
-                            }
-                        }
-                    }
-                    if constexpr (!PT) {
-                        f_hi = fs[0];
-                        if constexpr (LR) fu_hi = fus[0];
-                    }
-                };
-                auto body = [&](int c, auto R_, auto MASK_) {
-                    constexpr int r = decltype(R_)::value;
-                    constexpr int rn = (r + 1) & 3;
-                    CHUNKSTAMP(1, c);
-                    chunk(c, X[r], X[rn].pk, E[r & 1], BU[r & 1], E[(r + 1) & 1], BU[(r + 1) & 1], MASK_);
-                    if (c >= 4) X[r] = ldset(c - 4);
-                };
-                using Mk = std::integral_constant<bool, RAG>;  // only the first chunk is masked in full waves
-                body(cl, std::integral_constant<int, 0>{}, std::true_type{});  // holds t = Tw - 1
-                for (int c = cl - 1; c >= 0; c -= 4) {
-                    body(c, std::integral_constant<int, 1>{}, Mk{});
-                    if (c >= 1) body(c - 1, std::integral_constant<int, 2>{}, Mk{});
-                    if (c >= 2) body(c - 2, std::integral_constant<int, 3>{}, Mk{});
-                    if (c >= 3) body(c - 3, std::integral_constant<int, 0>{}, Mk{});
-                }
-            };
-            if (safe) {
-                if (full) backward(std::true_type{}, std::false_type{});
-                else backward(std::true_type{}, std::true_type{});
-            } else {
-                if (full) backward(std::false_type{}, std::false_type{});
-                else backward(std::false_type{}, std::true_type{});
-            }
-            gall += gex;
-            PHASE(3);
-            // xi_t(i,j) = a_ij * (the accumulated S_ij): scale once per sequence group (PT already
-            // accumulates xi itself)
-            if constexpr (!PT) {
-#pragma unroll
-                for (int k = 0; k < NS; ++k) {
-                    if constexpr (LR) S[k] *= (k == 0 ? a_dg : a_up);
-                    else S[k] *= arow[k];
-                }
-            }
-        }
-    }
-
-    // per-block (max, sum exp) of log P for the convergence scalar
-    __syncthreads();
-    block_ll_partial(logp_lane, ll_valid, sRed, a.llpart + 2 * (long long)blockIdx.x);
-    PHASE(4);
-
-    if constexpr (!FWD_ONLY) if (!(a.ablate & 1)) {
-        // ---- reduce per-lane accumulators over the U sequences of the wave, then the block ----
-        double vals[NV];
-#pragma unroll
-        for (int k = 0; k < NS; ++k) vals[k] = S[k];
-        vals[NS] = gex;
-        vals[NS + 1] = gall;
-        vals[NS + 2] = pin;
-#pragma unroll
-        for (int k = 0; k < NV; ++k) {
-            double x = vals[k];
-            for (int m = G; m < kWave; m <<= 1) x += __shfl_xor(x, m);
-            vals[k] = x;
-        }
-        __syncthreads();
-        if (u == 0) {
-#pragma unroll
-            for (int k = 0; k < NV; ++k) sRed[(wv * G + j) * NV + k] = vals[k];
-        }
-        __syncthreads();
-        const int nw = blockDim.x >> 6;
-        for (int idx = tid; idx < G * NV; idx += blockDim.x) {
-            const int jj = idx / NV, k = idx % NV;
-            if (jj >= N) continue;
-            double x = 0.0;
-            for (int w = 0; w < nw; ++w) x += sRed[(w * G + jj) * NV + k];
-            if (x == 0.0) continue;
-            long long dst;
-            if (k < NS) {
-                const int col = LR ? jj + k : k;
-                if (col >= N) continue;
-                dst = a.off_S + (long long)jj * N + col;
-            } else if (k == NS) {
-                dst = a.off_gex + jj;
-            } else if (k == NS + 1) {
-                dst = a.off_gall + jj;
-            } else {
-                dst = jj;  // pi_num at offset 0
-            }
-            unsafeAtomicAdd(&accb[dst], x);
-        }
-        if constexpr (LDSTAB) {
-            for (int idx = tid; idx < K * G; idx += blockDim.x) {
-                const int k = idx / G, jj = idx - k * G;
-                if (jj >= N) continue;
-                const double x = sBn[k * GP + jj];
-                if (x != 0.0) unsafeAtomicAdd(&accb[a.off_bnum + (long long)k * N + jj], x);
-            }
-        }
-    }
-    PHASE(5);
-}
-
-// ---------------------------------------------------------------------------------------------
-// Wide E-step / scorer: 16 < N <= 64, one sequence per wavefront, lane = state.
-// ---------------------------------------------------------------------------------------------
-template <int NP, bool FWD_ONLY>
-__global__ void __launch_bounds__(kBlock) k_estep_wide(EArgs a) {
-    extern __shared__ double smem[];
-    if (a.state != nullptr && a.state->done) return;
-    const int N = a.N;
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const int j = lane;
-    double *sA = smem;              // [NP][64]  a_ij at [i][j]
-    double *sAT = smem + NP * 64;   // [NP][64]  a_jk at [k][j]
-    double *sX = smem + 2 * NP * 64 + wv * 64;  // per-wave exchange row
-    for (int idx = tid; idx < NP * 64; idx += blockDim.x) {
-        const int r = idx / 64, c = idx % 64;
-        sA[idx] = (r < N && c < N) ? a.A[r * N + c] : 0.0;
-        sAT[idx] = (r < N && c < N) ? a.A[c * N + r] : 0.0;
-    }
-    __syncthreads();
-    const long long wave = (long long)blockIdx.x * (blockDim.x >> 6) + wv;
-    double *accb = a.copies + (long long)(blockIdx.x % a.ncopies) * a.copy_len;
-    double logp_lane = -INFINITY;
-    bool ll_valid = false;
-    [&]() {
-    if (wave >= a.L.nwaves) return;
-    const int T = a.L.slot_len[wave];
-    const int seq = a.L.slot_seq[wave];
-    if (T <= 0) return;
-    const int nch = (T + kChunk - 1) / kChunk;
-    const uint16_t *symw = a.L.sym + a.L.wave_symoff[wave];
-    double *aw = a.ckpt + (FWD_ONLY ? 0 : a.L.wave_ckoff[wave]) + lane;
-    int *ew = a.ebuf + (FWD_ONLY ? 0 : a.L.wave_spoff[wave]);
-    const bool jv = j < N;
-    const double pij = jv ? a.pi[j] : 0.0;
-    auto loadpack = [&](int c) -> uint4 { return *reinterpret_cast<const uint4 *>(symw + (long long)c * kChunk); };
-    auto xchg = [&](double v) {
-        __builtin_amdgcn_wave_barrier();
-        sX[lane] = v;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    };
-
-    double alpha = 0.0;
-    int E = 0;
-    uint4 pk = loadpack(0);
-    for (int c = 0; c < nch; ++c) {
-        const uint4 pkn = (c + 1 < nch) ? loadpack(c + 1) : pk;
-        for (int s = 0; s < kChunk; ++s) {
-            const int t = c * kChunk + s;
-            if (t >= T) break;
-            const int o = sym_of(pk, s);
-            const double b = a.Bt[(long long)o * 64 + j];
-            double x;
-            if (t == 0) {
-                x = pij * b;
-            } else {
-                xchg(alpha);
-                double acc0 = 0.0, acc1 = 0.0;
-#pragma unroll 8
-                for (int i = 0; i < NP; i += 2) {
-                    acc0 = fma(sX[i], sA[i * 64 + j], acc0);
-                    acc1 = fma(sX[i + 1], sA[(i + 1) * 64 + j], acc1);
-                }
-                x = (acc0 + acc1) * b;
-            }
-            const double sum = gsum<64>(x);
-            const int e = __builtin_amdgcn_frexp_exp(sum);
-            x = pow2_scale(x, e);
-            alpha = x;
-            E += e;
-            if constexpr (!FWD_ONLY) {
-                aw[(long long)t * kWave] = x;
-                if (j == 0) ew[t] = e;
-            }
-        }
-        pk = pkn;
-    }
-    const double phat = gsum<64>(alpha);
-    const bool alive = phat > 0.0;
-    const double lp = alive ? (log(phat) + (double)E * 0.69314718055994530942) : -INFINITY;
-    if (j == 0 && seq >= 0) a.logp[seq] = lp;
-    logp_lane = lp;
-    ll_valid = j == 0;
-    if constexpr (!FWD_ONLY) {
-        if (!alive) return;
-        double S[NP];
-#pragma unroll
-        for (int k = 0; k < NP; ++k) S[k] = 0.0;
-        double gex = 0.0, pin = 0.0;
-        double beta = 1.0 / phat;
-        auto symat = [&](int t) -> int { return symw[(long long)(t / kChunk) * kChunk + (t % kChunk)]; };
-        const double glast = alpha * beta;
-        double gall = glast;
-        if (T == 1) pin = glast;
-        if (jv) unsafeAtomicAdd(&accb[a.off_bnum + (long long)symat(T - 1) * N + j], glast);
-        int o1 = symat(T - 1);
-        for (int t = T - 2; t >= 0; --t) {
-            const int o0 = symat(t);
-            const double at = aw[(long long)t * kWave];
-            const int e1 = ew[t + 1];
-            const double b1 = a.Bt[(long long)o1 * 64 + j];
-            const double v = pow2_scale(b1 * beta, e1);
-            xchg(v);
-            double b0 = 0.0, bb = 0.0;
-#pragma unroll
-            for (int k = 0; k < NP; k += 2) {
-                const double v0 = sX[k], v1 = sX[k + 1];
-                b0 = fma(sAT[k * 64 + j], v0, b0);
-                bb = fma(sAT[(k + 1) * 64 + j], v1, bb);
-                S[k] = fma(at, v0, S[k]);
-                S[k + 1] = fma(at, v1, S[k + 1]);
-            }
-            const double bn = b0 + bb;
-            const double g = at * bn;
-            beta = bn;
-            gex += g;
-            if (t == 0) pin = g;
-            if (jv) unsafeAtomicAdd(&accb[a.off_bnum + (long long)o0 * N + j], g);
-            o1 = o0;
-        }
-        gall += gex;
-        if (jv) {
-#pragma unroll
-            for (int k = 0; k < NP; ++k)
-                if (k < N && S[k] != 0.0)  // xi_t(j,k) = a_jk * S_jk
-                    unsafeAtomicAdd(&accb[a.off_S + (long long)j * N + k], S[k] * sAT[k * 64 + j]);
-            if (gex != 0.0) unsafeAtomicAdd(&accb[a.off_gex + j], gex);
-            if (gall != 0.0) unsafeAtomicAdd(&accb[a.off_gall + j], gall);
-            if (pin != 0.0) unsafeAtomicAdd(&accb[j], pin);
-        }
-    }
-    }();
-    __syncthreads();
-    block_ll_partial(logp_lane, ll_valid, smem + 2 * NP * 64 + 4 * 64, a.llpart + 2 * (long long)blockIdx.x);
-}
-
-// ---------------------------------------------------------------------------------------------
-// Block reductions
-// ---------------------------------------------------------------------------------------------
-__device__ double block_reduce(double x, double *sh, bool is_max) {
-    const int tid = threadIdx.x;
-    for (int m = 32; m >= 1; m >>= 1) {
-        const double y = __shfl_xor(x, m);
-        x = is_max ? fmax(x, y) : x + y;
-    }
-    __syncthreads();
-    if ((tid & 63) == 0) sh[tid >> 6] = x;
-    __syncthreads();
-    if (tid < 64) {
-        const int nw = blockDim.x >> 6;
-        double y = tid < nw ? sh[tid] : (is_max ? -INFINITY : 0.0);
-        for (int m = 32; m >= 1; m >>= 1) {
-            const double z = __shfl_xor(y, m);
-            y = is_max ? fmax(y, z) : y + z;
-        }
-        if (tid == 0) sh[0] = y;
-    }
-    __syncthreads();
-    const double r = sh[0];
-    __syncthreads();
-    return r;
-}
-
-// Combine per-block (max, sum exp) pairs into this rank's pair (log_sum_exp :66-79 over :503).
-// ATOMIC: read with returning memory-side atomics (inside the producing kernel, where the per-XCD
-// L2s give no cross-workgroup visibility for plain loads).
-template <bool ATOMIC = false>
-__device__ __forceinline__ double rd(const double *p) {
-    if constexpr (ATOMIC) return unsafeAtomicAdd(const_cast<double *>(p), 0.0);
-    else return *p;
-}
-
-template <bool ATOMIC = false>
-__device__ void combine_ll_pairs(const double *pairs, long long n, double *sh, double *m_out, double *s_out) {
-    double mx = -INFINITY;
-    for (long long r = threadIdx.x; r < n; r += blockDim.x)
-        if (rd<ATOMIC>(&pairs[2 * r + 1]) > 0.0) mx = fmax(mx, rd<ATOMIC>(&pairs[2 * r]));
-    mx = block_reduce(mx, sh, true);
-    double s = 0.0;
-    if (mx != -INFINITY)
-        for (long long r = threadIdx.x; r < n; r += blockDim.x) {
-            const double sr = rd<ATOMIC>(&pairs[2 * r + 1]);
-            if (sr > 0.0) s += sr * exp(rd<ATOMIC>(&pairs[2 * r]) - mx);
-        }
-    s = block_reduce(s, sh, false);
-    *m_out = mx;
-    *s_out = s;
-}
 
 // Multi-rank: sum this rank's statistics copies into the caller's buffer (for the all-reduce),
 // zero the copies, and write the rank's (max, sum exp) pair of log P into its slot.
@@ -1004,403 +63,9 @@ __global__ void __launch_bounds__(256) k_reduce_local(double *copies, int ncopie
     }
 }
 
-
-// sum of one statistic over the copies, clearing them for the next iteration
-template <bool ATOMIC>
-__device__ __forceinline__ double take(const MArgs &m, long long idx) {
-    double v = 0.0;
-    double *p = const_cast<double *>(m.src) + idx;
-    for (int c = 0; c < m.nsrc; ++c) {
-        if constexpr (ATOMIC) {
-            v += atomicExch(p + c * m.copy_len, 0.0);
-        } else {
-            v += p[c * m.copy_len];
-            p[c * m.copy_len] = 0.0;
-        }
-    }
-    return v;
-}
-
-// B entry from its numerator and the reciprocal of its row's denominator (:460-497): 1e-20 floor when
-// no gamma term carries the symbol, 0 for an empty row.  Shared by every M-step variant, so they
-// produce bit-identical parameters.
-__device__ __forceinline__ double mstep_inv(double den) { return den > 0.0 ? 1.0 / den : 0.0; }
-__device__ __forceinline__ double bnum_to_b(double num, double inv) {
-    return inv > 0.0 ? (num > 0.0 ? num * inv : 1e-20) : 0.0;
-}
-
-// Convergence record of one EM iteration (hmm_training.py:503-514): L of the parameters that entered
-// it, diff (+inf on the first iteration), the stop rule of :346; written to the next state slot.
-__device__ bool record_iteration(const MArgs &m, const IterState &in, double L) {
-    const double diff = (in.prev_L != -INFINITY) ? fabs(L - in.prev_L) : INFINITY;  // :505-508
-    const long long it = in.iteration;
-    const bool cont = (diff >= in.epsilon) && (it + 1 < in.max_iterations);
-    m.hist[2 * (it % kHist)] = L;
-    m.hist[2 * (it % kHist) + 1] = diff;
-    IterState o = in;
-    o.prev_L = L;
-    o.last_L = L;
-    o.last_diff = diff;
-    o.iteration = it + 1;
-    if (!cont) {
-        o.done = 1;
-        o.converged = (it + 1 < in.max_iterations) ? 1 : 0;
-    }
-    *m.state_out = o;
-    return cont;
-}
-
-// M-step kernels entered after convergence carry the state over to the next slot and do nothing else
-__device__ __forceinline__ bool carry_if_done(const MArgs &m) {
-    if (!m.state->done) return false;
-    if (threadIdx.x == 0 && blockIdx.x == 0) *m.state_out = *m.state;
-    return true;
-}
-
-// M-step + convergence by one workgroup of 256 threads (hmm_training.py:415-514).
-template <bool ATOMIC>
-__device__ void mstep_block(const MArgs &m) {
-    __shared__ double sh[16];
-    __shared__ double sL;
-    __shared__ double sPi[64], sGex[64], sGall[64];
-    const IterState *st = m.state;
-    const int tid = threadIdx.x;
-    // L = LSE_r log P_r over all ranks (:503)
-    if (m.local_lse) {
-        double mx, s;
-        combine_ll_pairs<ATOMIC>(m.llpart, m.nblocks, sh, &mx, &s);
-        if (tid == 0) sL = (s > 0.0) ? mx + log(s) : -INFINITY;
-    } else if (tid == 0) {
-        const double *ll = m.src + m.off_ll;
-        double mx = -INFINITY;
-        for (int r = 0; r < m.world; ++r)
-            if (ll[2 * r + 1] > 0.0) mx = fmax(mx, ll[2 * r]);
-        double s = 0.0;
-        if (mx != -INFINITY)
-            for (int r = 0; r < m.world; ++r)
-                if (ll[2 * r + 1] > 0.0) s += ll[2 * r + 1] * exp(ll[2 * r] - mx);
-        sL = (s > 0.0) ? mx + log(s) : -INFINITY;
-        for (int r = 0; r < 2 * m.world; ++r) m.zero_ll[r] = 0.0;
-    }
-    const int N = m.N, K = m.K;
-    for (int i = tid; i < N; i += blockDim.x) {
-        sPi[i] = take<ATOMIC>(m, i);
-        sGex[i] = take<ATOMIC>(m, m.off_gex + i);
-        sGall[i] = take<ATOMIC>(m, m.off_gall + i);
-    }
-    __syncthreads();
-    // pi (:415-424): LSE_r gamma_0 - log R ; no term -> -inf
-    for (int i = tid; i < N; i += blockDim.x) m.pi[i] = sPi[i] > 0.0 ? sPi[i] / (double)m.R_global : 0.0;
-    // A (:429-455): xi numerator; denominator excludes the last frame
-    for (int idx = tid; idx < N * N; idx += blockDim.x) {
-        const double den = sGex[idx / N];
-        const double num = take<ATOMIC>(m, m.off_S + idx);
-        m.A[idx] = (den > 0.0 && num > 0.0) ? num / den : 0.0;
-    }
-    // B (:460-497): floor 1e-20 when no gamma term carries the symbol; empty denominator -> row 0
-    for (long long idx = tid; idx < (long long)N * K; idx += blockDim.x) {
-        const int jj = (int)(idx % N), k = (int)(idx / N);  // symbol-major: coalesced over the copies
-        const double num = take<ATOMIC>(m, m.off_bnum + idx);
-        const double v = bnum_to_b(num, mstep_inv(sGall[jj]));
-        m.B[(long long)jj * K + k] = v;
-        m.Bt[(long long)k * m.G + jj] = v;
-    }
-    __syncthreads();
-    if (tid == 0) record_iteration(m, *st, sL);
-}
-
 __global__ void __launch_bounds__(256) k_mstep(MArgs m) {
     if (carry_if_done(m)) return;
     mstep_block<false>(m);
-}
-
-
-// merge (max, sum exp) pairs: online log-sum-exp
-__device__ __forceinline__ void ll_merge(double &M, double &S, double m2, double s2) {
-    if (!(s2 > 0.0)) return;
-    if (!(S > 0.0)) { M = m2; S = s2; return; }
-    if (m2 > M) { S = S * exp(M - m2) + s2; M = m2; }
-    else S += s2 * exp(m2 - M);
-}
-
-// M-step staged through LDS (sSt: copy_len doubles): the statistics (summed over the copies, which
-// are cleared) and the per-workgroup log-likelihood pairs are gathered in independent batches, then
-// the update runs from LDS.  ATOMIC (fused into the E-step): gathered with returning memory-side
-// atomics; otherwise (its own kernel, after a kernel boundary) with plain loads.
-template <bool ATOMIC>
-__device__ void mstep_staged(const MArgs &m, double *sSt) {
-    __shared__ double sM[16], sS[16];
-    __shared__ double sL;
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, nw = blockDim.x >> 6;
-    const int N = m.N, K = m.K;
-    const long long len = m.copy_len;
-    // ---- one batch of independent loads: convergence state, LL pairs, statistics ----
-    IterState in{};
-    if (tid == 0) in = *m.state;
-    // Branch-free, clamped addresses so the compiler issues every load of a batch before the first
-    // wait (a guarded load inside a runtime loop serialises on its own s_waitcnt).
-    constexpr int PB = 4;
-    double pm[PB], ps[PB];
-    double M = -INFINITY, S = 0.0;
-    const long long nb = m.nblocks;  // >= 1 (a launch with no workgroups leaves nothing pending)
-    for (long long r0 = 0; r0 < nb; r0 += (long long)PB * blockDim.x) {
-#pragma unroll
-        for (int u = 0; u < PB; ++u) {
-            const long long r = r0 + (long long)u * blockDim.x + tid;
-            const long long rc = r < nb ? r : nb - 1;
-            pm[u] = rd<ATOMIC>(m.llpart + 2 * rc);
-            ps[u] = rd<ATOMIC>(m.llpart + 2 * rc + 1);
-        }
-#pragma unroll
-        for (int u = 0; u < PB; ++u) {
-            const bool ok = r0 + (long long)u * blockDim.x + tid < nb;
-            ll_merge(M, S, ok ? pm[u] : -INFINITY, ok ? ps[u] : 0.0);
-        }
-    }
-    constexpr int B = 16;
-    double *src = const_cast<double *>(m.src);
-    for (long long base = 0; base < len; base += (long long)B * blockDim.x) {
-        double v[B];
-#pragma unroll
-        for (int u = 0; u < B; ++u) v[u] = 0.0;
-        for (int c = 0; c < m.nsrc; ++c) {
-            double x[B];
-#pragma unroll
-            for (int u = 0; u < B; ++u) {
-                const long long idx = base + (long long)u * blockDim.x + tid;
-                double *q = src + c * len + (idx < len ? idx : len - 1);
-                if constexpr (ATOMIC) x[u] = idx < len ? atomicExch(q, 0.0) : 0.0;
-                else x[u] = *q;
-            }
-#pragma unroll
-            for (int u = 0; u < B; ++u) v[u] += x[u];
-        }
-#pragma unroll
-        for (int u = 0; u < B; ++u) {
-            const long long idx = base + (long long)u * blockDim.x + tid;
-            if (idx < len) {
-                sSt[idx] = v[u];
-                if constexpr (!ATOMIC)
-                    for (int c = 0; c < m.nsrc; ++c) src[c * len + idx] = 0.0;
-            }
-        }
-    }
-    // ---- L = LSE_r log P_r (:503) ----
-    for (int k = 32; k >= 1; k >>= 1) ll_merge(M, S, __shfl_xor(M, k), __shfl_xor(S, k));
-    if (lane == 0) { sM[wv] = M; sS[wv] = S; }
-    __syncthreads();
-    if (tid == 0) {
-        double MM = -INFINITY, SS = 0.0;
-        for (int w = 0; w < nw; ++w) ll_merge(MM, SS, sM[w], sS[w]);
-        sL = (SS > 0.0) ? MM + log(SS) : -INFINITY;
-    }
-    __syncthreads();
-    const double *sPi = sSt, *sS_ = sSt + m.off_S, *sGex = sSt + m.off_gex, *sGall = sSt + m.off_gall,
-                 *sBn = sSt + m.off_bnum;
-    // pi (:415-424), A (:429-455), B (:460-497)
-    if (tid < N) m.pi[tid] = sPi[tid] > 0.0 ? sPi[tid] / (double)m.R_global : 0.0;
-    if (tid < N * N) {
-        const double den = sGex[tid / N];
-        const double num = sS_[tid];
-        m.A[tid] = (den > 0.0 && num > 0.0) ? num / den : 0.0;
-    }
-    for (int idx = tid; idx < N * K; idx += blockDim.x) {
-        const int k = idx / N, jj = idx - k * N;
-        const double v = bnum_to_b(sBn[idx], mstep_inv(sGall[jj]));
-        m.B[(long long)jj * K + k] = v;
-        m.Bt[(long long)k * m.G + jj] = v;
-    }
-    if (tid == 0) record_iteration(m, in, sL);
-}
-
-// The previous iteration's M-step + convergence step (hmm_training.py:415-514), run by EVERY
-// workgroup of the merged E-step launch, straight into its LDS tables: every workgroup reads the same
-// statistics and log-likelihood pairs and applies the same arithmetic in the same order, so all of
-// them hold bit-identical parameters and reach the same stop decision.  Workgroup 0 also writes the
-// parameters back to HBM (for the queries) and records the iteration in the other state slot.
-// Returns false when EM stops here (or had stopped before).
-constexpr int kMergedMaxStats = 16 * kBlock;  // statistics per launch the prologue holds in registers
-
-__device__ __forceinline__ double wave_max(double x) {
-    x = fmax(x, dpp<0xB1>(x));
-    x = fmax(x, dpp<0x4E>(x));
-    x = fmax(x, dpp<0x141>(x));
-    x = fmax(x, dpp<0x140>(x));
-    x = fmax(x, __shfl_xor(x, 16));
-    return fmax(x, __shfl_xor(x, 32));
-}
-
-template <int N, int G, int GP, bool HIST, bool PT>
-__device__ bool merged_mstep(const EArgs &a, double *sBt, double2 *sBP, double *sBn, double *sPA) {
-    constexpr int NSM = N + N * N + 2 * N;  // pi_num, xi, gamma_den_excl, gamma_den_all
-    constexpr int NW = kBlock / 64;
-    constexpr int SB = kMergedMaxStats / kBlock;
-    constexpr int PB = 2;                   // log-likelihood pairs per thread per pass
-    __shared__ double sSm[NSM];
-    __shared__ double sMx[NW], sSum[NW];
-    __shared__ IterState sIn;
-    const MArgs &m = a.m;
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const int K = a.K;
-    const long long len = m.copy_len;
-    // ---- every load issued before any use: statistics, log-likelihood pairs, convergence state ----
-    double v[SB];
-#pragma unroll
-    for (int q = 0; q < SB; ++q) {
-        const long long idx = (long long)q * kBlock + tid;
-        v[q] = m.src[idx < len ? idx : len - 1];
-    }
-    for (int c = 1; c < m.nsrc; ++c) {
-        double x[SB];
-#pragma unroll
-        for (int q = 0; q < SB; ++q) {
-            const long long idx = (long long)q * kBlock + tid;
-            x[q] = m.src[c * len + (idx < len ? idx : len - 1)];
-        }
-#pragma unroll
-        for (int q = 0; q < SB; ++q) v[q] += x[q];
-    }
-    const long long nb = m.nblocks;  // >= 1
-    double pm[PB], ps[PB];
-#pragma unroll
-    for (int q = 0; q < PB; ++q) {
-        const long long r = (long long)q * kBlock + tid;
-        const long long rc = r < nb ? r : nb - 1;
-        pm[q] = m.llpart[2 * rc];
-        ps[q] = m.llpart[2 * rc + 1];
-    }
-    IterState in{};
-    if (tid == 0) {
-        in.prev_L = m.state->prev_L;
-        in.epsilon = m.state->epsilon;
-        in.iteration = m.state->iteration;
-        in.max_iterations = m.state->max_iterations;
-        in.done = m.state->done;
-        in.converged = m.state->converged;
-        in.last_L = m.state->last_L;
-        in.last_diff = m.state->last_diff;
-    }
-    // ---- L = LSE_r log P_r (:503) in two passes: max, then sum of exp(m - max) ----
-    double mx = -INFINITY;
-#pragma unroll
-    for (int q = 0; q < PB; ++q) {
-        const bool ok = (long long)q * kBlock + tid < nb && ps[q] > 0.0;
-        mx = ok ? fmax(mx, pm[q]) : mx;
-    }
-    for (long long r = (long long)PB * kBlock + tid; r < nb; r += kBlock)  // > 512 workgroups
-        if (m.llpart[2 * r + 1] > 0.0) mx = fmax(mx, m.llpart[2 * r]);
-    mx = wave_max(mx);
-    if (lane == 0) sMx[wv] = mx;
-#pragma unroll
-    for (int q = 0; q < SB; ++q) {
-        const int idx = q * kBlock + tid;
-        if (idx < NSM) sSm[idx] = (idx < len) ? v[q] : 0.0;
-    }
-    if (tid == 0) sIn = in;
-    __syncthreads();
-    PHASE(6);
-    if (sIn.done) {  // converged before this launch: device-side no-op
-        if (tid == 0 && blockIdx.x == 0) *m.state_out = sIn;
-        return false;
-    }
-    double Mb = sMx[0];
-#pragma unroll
-    for (int w = 1; w < NW; ++w) Mb = fmax(Mb, sMx[w]);
-    double sum = 0.0;
-    if (Mb != -INFINITY) {
-#pragma unroll
-        for (int q = 0; q < PB; ++q) {
-            const bool ok = (long long)q * kBlock + tid < nb && ps[q] > 0.0;
-            sum += ok ? ps[q] * exp(pm[q] - Mb) : 0.0;
-        }
-        for (long long r = (long long)PB * kBlock + tid; r < nb; r += kBlock)
-            if (m.llpart[2 * r + 1] > 0.0) sum += m.llpart[2 * r + 1] * exp(m.llpart[2 * r] - Mb);
-    }
-    sum = gsum<64>(sum);
-    if (lane == 0) sSum[wv] = sum;
-    PHASE(7);
-    // pi (:415-424), A (:429-455) into LDS
-    if (tid < G) sPA[tid] = (tid < N && sSm[tid] > 0.0) ? sSm[tid] / (double)m.R_global : 0.0;
-    if (tid < N * N) {
-        const double den = sSm[N + N * N + tid / N];
-        const double num = sSm[N + tid];
-        sPA[G + tid] = (den > 0.0 && num > 0.0) ? num / den : 0.0;
-    }
-    // B (:460-497) from the registers straight into the emission table (and HBM, workgroup 0).
-    // Element e = q * kBlock + tid - NSM is symbol e / N, state e % N; with N | kBlock the state (and
-    // so the denominator) is the same for every q of a thread: one reciprocal per thread.
-    const bool w0 = blockIdx.x == 0;
-    const int e0 = tid - NSM;
-    constexpr bool kSameState = (kBlock % N) == 0;
-    const int jj0 = ((e0 % N) + N) % N;
-    const double inv0 = kSameState ? mstep_inv(sSm[N + N * N + N + jj0]) : 0.0;
-    // PT: a_jj and a_{j-1,j} of the element's state, the same arithmetic as sPA's A (:429-455)
-    auto a_of = [&](int r, int c) -> double {
-        const double den = sSm[N + N * N + r];
-        const double num = sSm[N + r * N + c];
-        return (den > 0.0 && num > 0.0) ? num / den : 0.0;
-    };
-    double ad0 = 0.0, ai0 = 0.0;
-    if constexpr (PT && kSameState) {
-        ad0 = a_of(jj0, jj0);
-        ai0 = jj0 >= 1 ? a_of(jj0 - 1, jj0) : 0.0;
-    }
-    double bval[SB];
-#pragma unroll
-    for (int q = 0; q < SB; ++q) {
-        const int e = q * kBlock + e0;
-        const int jj = kSameState ? jj0 : ((e % N) + N) % N;
-        const double inv = kSameState ? inv0 : mstep_inv(sSm[N + N * N + N + jj]);
-        bval[q] = bnum_to_b(v[q], inv);
-        if (e >= 0 && e < K * N) {
-            sBt[(e / N) * GP + jj] = bval[q];
-            if constexpr (PT) {
-                const double ad = kSameState ? ad0 : a_of(jj, jj);
-                const double ai = kSameState ? ai0 : (jj >= 1 ? a_of(jj - 1, jj) : 0.0);
-                sBP[(e / N) * GP + jj] = double2{ad * bval[q], ai * bval[q]};
-            }
-        }
-    }
-    if (w0) {
-#pragma unroll
-        for (int q = 0; q < SB; ++q) {
-            const int e = q * kBlock + e0;
-            if (e >= 0 && e < K * N) {
-                const int k = e / N, jj = e - k * N;
-                m.B[(long long)jj * K + k] = bval[q];
-                m.Bt[(long long)k * G + jj] = bval[q];
-            }
-        }
-    }
-    // zero the pad columns [N, GP) of every row and the pad row K; clear the histogram
-    for (int i = tid; i < (K + 1) * (GP - N); i += kBlock) {
-        const int k = i / (GP - N), c = N + (i - k * (GP - N));
-        sBt[k * GP + c] = 0.0;
-        if constexpr (PT) sBP[k * GP + c] = double2{0.0, 0.0};
-    }
-    if (tid < N) {
-        sBt[K * GP + tid] = 0.0;
-        if constexpr (PT) sBP[K * GP + tid] = double2{0.0, 0.0};
-    }
-    if constexpr (HIST) {
-        double2 *z2 = reinterpret_cast<double2 *>(sBn);
-        for (int i = tid; i < K * GP / 2; i += kBlock) z2[i] = double2{0.0, 0.0};
-        if ((K * GP) & 1)
-            if (tid == 0) sBn[K * GP - 1] = 0.0;
-    }
-    __syncthreads();
-    double S = 0.0;
-#pragma unroll
-    for (int w = 0; w < NW; ++w) S += sSum[w];
-    const double L = (S > 0.0) ? Mb + log(S) : -INFINITY;
-    const double diff = (sIn.prev_L != -INFINITY) ? fabs(L - sIn.prev_L) : INFINITY;  // :505-508
-    const bool cont = (diff >= sIn.epsilon) && (sIn.iteration + 1 < sIn.max_iterations);  // :346
-    if (w0) {
-        if (tid < N) m.pi[tid] = sPA[tid];
-        if (tid < N * N) m.A[tid] = sPA[G + tid];
-        if (tid == 0) record_iteration(m, sIn, L);
-    }
-    return cont;
 }
 
 // single-rank M-step with the statistics staged in dynamic LDS (copy_len doubles)
@@ -1471,28 +136,12 @@ void dfree(T *&p) {
     p = nullptr;
 }
 
-using KernelFn = void (*)(EArgs);
-
-struct Kernels {
-    KernelFn estep = nullptr, score = nullptr;
-};
-
-template <int N, int G, bool LR, bool LDSTAB>
-Kernels small_kernels() {
-    return Kernels{k_estep_small<N, G, LR, LDSTAB, false>, k_estep_small<N, G, LR, LDSTAB, true>};
-}
-
-template <int N, bool LR, bool LDSTAB>
-Kernels pick_small_g() {
-    constexpr int G = N <= 2 ? 2 : (N <= 4 ? 4 : (N <= 8 ? 8 : 16));
-    return small_kernels<N, G, LR, LDSTAB>();
-}
-
+// E-step kernel pointers live in the instantiation units (hmmbw_kernels.hpp)
 template <bool LR, bool LDSTAB>
 Kernels pick_small_n(int N) {
     switch (N) {
 #define CASE(n) \
-    case n: return pick_small_g<n, LR, LDSTAB>();
+    case n: return small_kernels_n<n>(LR, LDSTAB);
         CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8)
         CASE(9) CASE(10) CASE(11) CASE(12) CASE(13) CASE(14) CASE(15) CASE(16)
 #undef CASE
@@ -1713,8 +362,8 @@ int launch_estep(hmmbw_ctx *c, bool fwd_only, const IterState *state, double *co
     }
     if (c->wide) {
         const size_t lds = sizeof(double) * (2 * (size_t)c->NP * 64 + (size_t)wpb * 64 + 8);
-        KernelFn f = c->NP == 32 ? (fwd_only ? k_estep_wide<32, true> : k_estep_wide<32, false>)
-                                 : (fwd_only ? k_estep_wide<64, true> : k_estep_wide<64, false>);
+        const Kernels kw = wide_kernels(c->NP);
+        KernelFn f = fwd_only ? kw.score : kw.estep;
         if (int rc = launch_lds(f, grid, lds, c->stream, a)) return rc;
     } else {
         const bool lr = c->topo == HMMBW_TOPOLOGY_LEFT_TO_RIGHT;
@@ -2204,20 +853,5 @@ int hmmbw_timing(hmmbw_ctx *c, int enable, double *total_ms, int64_t *count) {
     return HMMBW_OK;
 }
 
-#ifdef HMMBW_PHASE_TIMES
-int hmmbw_debug_phase_times(unsigned long long *out, int64_t nwaves) {
-    if (!out || nwaves < 0 || nwaves > kPhaseWaves) return fail(HMMBW_E_INVALID, "bad argument");
-    HIP_TRY(hipDeviceSynchronize());
-    HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase), sizeof(unsigned long long) * 8 * nwaves));
-    return HMMBW_OK;
-}
-
-int hmmbw_debug_chunk_times(unsigned long long *out, int64_t nwaves) {
-    if (!out || nwaves < 0 || nwaves > 4096) return fail(HMMBW_E_INVALID, "bad argument");
-    HIP_TRY(hipDeviceSynchronize());
-    HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_chunk), sizeof(unsigned long long) * 128 * nwaves));
-    return HMMBW_OK;
-}
-#endif
 
 }  // extern "C"

@@ -1,0 +1,27 @@
+// hmmbw_kernels.hpp — E-step kernel entry points exported by the instantiation units.
+//
+// The small-N kernel k_estep_small<N, G, LR, LDSTAB, FWD_ONLY> has 128 instantiations (N = 1..16 x
+// topology x LDS tables x E-step/scorer); each N lives in its own translation unit
+// (estep_small_inst.hip compiled with -DHMMBW_INST_N=n) so the build compiles them in parallel.
+// The pointers returned here are the kernels' host stubs, registered by their own unit's module.
+#pragma once
+
+#include "hmmbw_device.hpp"
+
+namespace hmmbw {
+
+using KernelFn = void (*)(EArgs);
+
+struct Kernels {
+    KernelFn estep = nullptr, score = nullptr;
+};
+
+// E-step and scorer kernels for N states (1 <= N <= 16), left-to-right or dense, with or without the
+// LDS emission tables.
+template <int N>
+Kernels small_kernels_n(bool lr, bool ldstab);
+
+// Wide kernels (16 < N <= 64) for the padded state count NP (32 or 64).
+Kernels wide_kernels(int NP);
+
+}  // namespace hmmbw

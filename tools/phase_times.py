@@ -33,7 +33,7 @@ def main():
     os.makedirs(out_dir, exist_ok=True)
     lib = os.path.join(out_dir, "libhmmbw_phase.so")
     from hmm_training_amd import build as B
-    subprocess.run([B.HIPCC, *B.FLAGS, "-DHMMBW_PHASE_TIMES", B.SRC, "-o", lib], check=True)
+    B.build(force=True, defines=["-DHMMBW_PHASE_TIMES"], out=lib, tag="phase")
     os.environ["HMMBW_LIB"] = lib
     import torch
     from hmm_training_amd.engine import BaumWelchEngine
