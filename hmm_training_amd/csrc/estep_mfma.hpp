@@ -1,0 +1,375 @@
+// estep_mfma.hpp — E-step / scorer for 16 < N <= 64 states on the fp64 matrix cores (gfx950).
+//
+// Replaces the per-utterance forward / backward loops of HMM/hmm_training.py:351-410
+// (calculate_log_alpha :122-160, calculate_log_beta :163-199, gamma :388-394, xi :396-410) and the
+// forward-only scorer of HMM/hmm_testing.py:49-104 for the dense large-state models (BASELINE cfg5:
+// N=64, K=1024, T=400).
+//
+// Mapping.  A workgroup owns a TILE of 16 sequences (the MFMA column dimension) and has NT = NP/16
+// waves; wave m owns the 16-state block [16m, 16m+16) of the (zero-padded) state vector.  With
+// v_mfma_f64_16x16x4_f64 (C/D: col = lane&15, row = (lane>>4) + 4*reg; A/B one f64 per lane, A[l&15][l>>4],
+// B[l>>4][l&15]) a 16x16 block of Z^T = [state][sequence] in C/D form is exactly the B operand of the
+// next product over states, so the recursions never move data across lanes:
+//   forward   Zt^T[o, s] = sum_i A[i][o] Z_{t-1}^T[i, s]           (16-state block m: 4NT MFMAs)
+//   backward  beta_t[i, s] = sum_j A[i][j] V_{t+1}[j, s]            (4NT MFMAs)
+//   xi        S[i][j] += sum_s z_t[i, s] V_{t+1}[j, s]               (NT x 4 MFMAs: k = sequence)
+// Lane (s = lane&15, g = lane>>4) holds states 16m + g + 4r (r = 0..3) of sequence s.  The blocks of
+// the other waves come through a double-buffered LDS image [state][16] (row stride 17 doubles: both the
+// C/D-form and the transposed reads of the xi operands are bank-conflict free), one s_barrier per step.
+//
+// Numerics (same scaled-linear fp64 scheme as the small kernel): z_t = x_t 2^{-s_t} with
+// the exact power-of-two s_t = (largest biased exponent of z_{t-1} over the sequence's states) - 1023,
+// so z stays within one step's growth of 1 (no lag, no fallback needed); log P = log(sum z_{T-1}) +
+// ln2 * sum s_t; the backward uses Rabiner scaling with the same s_t.  alpha_hat (fp64) and s_t go to
+// HBM in the forward and come back in the backward (the recursions here are bound by the fp64 matrix
+// rate, not by these bytes).
+//
+// B numerator (:474-485).  With K = 1024 symbols x 64 states the per-symbol histogram (512 KB) cannot
+// live in LDS, and scattering every gamma_t(j) into it with global fp64 atomics costs more than the
+// whole forward.  Instead each gamma row (one position, NP states, bt_col order) is stored once to a
+// per-position buffer, and k_bnum_gather (one workgroup per symbol, the host's symbol -> positions
+// index) sums the rows of each symbol: deterministic, and HBM-streaming rather than atomic-bound.
+#pragma once
+
+#include "hmmbw_device.hpp"
+
+namespace hmmbw {
+
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kTileSeqs = 16;  // sequences per tile = MFMA columns
+constexpr int kXs = 17;        // LDS row stride (doubles) of a [state][16 sequences] image
+
+__device__ __forceinline__ f64x4 mfma_f64(double a, double b, f64x4 c) {
+    return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+
+template <int NT, bool FWD_ONLY>
+__global__ void __launch_bounds__(NT * 64) k_estep_mfma(EArgs a) {
+    constexpr int NP = 16 * NT, KB = 4 * NT, IMG = NP * kXs;
+    extern __shared__ double smem[];
+    double *X0 = smem;                                   // [2][NP][kXs]: z (forward) / V (backward)
+    double *X1 = smem + 2 * IMG;                         // [2][NP][kXs]: masked z (backward xi operand)
+    double *sRed = smem + (FWD_ONLY ? 2 : 4) * IMG;      // [NT][16] partial sums + block LL scratch
+    if (a.state != nullptr && a.state->done) return;    // converged: device-side no-op (:346)
+    const int tid = threadIdx.x, lane = tid & 63, m = tid >> 6;
+    const int s = lane & 15, g = lane >> 4;
+    const int N = a.N;
+    const long long tile = blockIdx.x;
+    const long long slot = tile * kTileSeqs + s;
+    const int T = a.L.slot_len[slot];
+    const int seq = a.L.slot_seq[slot];
+    const int Tw = a.L.wave_T[tile];
+    const bool full = a.L.wave_full[tile] != 0;          // every sequence of the tile has length Tw
+    const int nch = (Tw + kChunk - 1) / kChunk;
+    const uint16_t *symw = a.L.sym + a.L.wave_symoff[tile] + s * kChunk;
+    double *ckw = a.ckpt + (FWD_ONLY ? 0 : a.L.wave_ckoff[tile]) + (long long)m * 4 * 64 + lane;
+    int *ew = a.ebuf + (FWD_ONLY ? 0 : a.L.wave_spoff[tile]) + s;
+    const int col0 = 16 * m + 4 * g;  // this lane's 4 emission columns (bt_col order)
+    // gamma row of position (t, s): gw + t * 16 * NP, this lane's 4 columns
+    double *gw = a.gam + (FWD_ONLY ? 0 : a.L.wave_ckoff[tile]) + (long long)s * NP + col0;
+    auto putg = [&](int t, const f64x4 &v) {
+        double2 *q = reinterpret_cast<double2 *>(gw + (long long)t * kTileSeqs * NP);
+        q[0] = double2{v[0], v[1]};
+        q[1] = double2{v[2], v[3]};
+    };
+
+    auto loadpack = [&](int c) -> uint4 {
+        return *reinterpret_cast<const uint4 *>(symw + (long long)c * kTileSeqs * kChunk);
+    };
+    auto emis = [&](int o) -> f64x4 {  // b_j(o) for j = 16m + g + 4r, r = 0..3
+        const double2 *p = reinterpret_cast<const double2 *>(a.Bt + (long long)o * NP + col0);
+        const double2 lo = p[0], hi = p[1];
+        return f64x4{lo.x, lo.y, hi.x, hi.y};
+    };
+    // this wave's block of a [state][16] LDS image (C/D form), the B operand of k-block kb, and the
+    // transposed read [state 16mm + (lane & 15)][sequence 4kk + (lane >> 4)] (the xi operands)
+    double *const putb = X0 + (16 * m + g) * kXs + s;
+    auto put = [&](double *base, int p, const f64x4 &v) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) base[p * IMG + 4 * r * kXs] = v[r];
+    };
+    const double *const bopb = X0 + g * kXs + s;
+    const double *const topb = X0 + (lane & 15) * kXs + (lane >> 4);
+    auto bexp = [](double x) -> int { return (int)__builtin_amdgcn_ubfe((unsigned)__double2hiint(x), 20, 11); };
+    // sum over the 16 sequences of a 16-lane row
+    auto rowsum = [](double x) -> double {
+#pragma unroll
+        for (int q = 1; q < kTileSeqs; q <<= 1) x += __shfl_xor(x, q);
+        return x;
+    };
+
+    // forward A operands of this wave's 16-state block: A^T[o][i] = a_io (o = 16m + (lane&15),
+    // i = 4kb + (lane>>4))
+    double aop[KB];
+#pragma unroll
+    for (int kb = 0; kb < KB; ++kb) {
+        const int o = 16 * m + (lane & 15), i = 4 * kb + (lane >> 4);
+        aop[kb] = (i < N && o < N) ? a.A[i * N + o] : 0.0;
+    }
+
+    // ---------------- forward (hmm_training.py:357-368; hmm_testing.py:70-92) ----------------
+    f64x4 z = {0.0, 0.0, 0.0, 0.0};
+    int C = 0;
+    f64x4 bring[2];  // b(o_t) in slot t % 2, loaded one step ahead
+    bring[0] = emis(sym_of(loadpack(0), 0));
+    auto fstep = [&](int t, const f64x4 &b, auto MASK_) {
+        constexpr bool MASK = decltype(MASK_)::value;
+        f64x4 x;
+        int sc = 0;
+        if (t == 0) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int j = 16 * m + g + 4 * r;
+                x[r] = (j < N && T > 0) ? a.pi[j] * b[r] : 0.0;  // pi_j b_j(o_0) (:357-360)
+            }
+        } else {
+            const double *src = bopb + ((t - 1) & 1) * IMG;
+            double zb[KB];
+#pragma unroll
+            for (int kb = 0; kb < KB; ++kb) zb[kb] = src[4 * kb * kXs];
+            f64x4 acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int kb = 0; kb < KB; kb += 2) {
+                acc0 = mfma_f64(aop[kb], zb[kb], acc0);
+                acc1 = mfma_f64(aop[kb + 1], zb[kb + 1], acc1);
+            }
+            // s_t from z_{t-1} over all NP states of the sequence (4 lanes x KB values)
+            int M = 0;
+#pragma unroll
+            for (int kb = 0; kb < KB; ++kb) M = max(M, bexp(zb[kb]));
+            M = max(M, __shfl_xor(M, 16));
+            M = max(M, __shfl_xor(M, 32));
+            sc = M == 0 ? 0 : M - 1023;
+            // rescale before the emission factor: z_{t-1} and b(o_t) may both be ~1e-200 (no underflow)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) x[r] = __builtin_amdgcn_ldexp(acc0[r] + acc1[r], -sc) * b[r];
+        }
+        if constexpr (MASK) {
+            const bool act = t < T;  // past the sequence's end: z frozen at z_{T-1}
+#pragma unroll
+            for (int r = 0; r < 4; ++r) z[r] = act ? x[r] : z[r];
+            sc = act ? sc : 0;
+        } else {
+            z = x;
+        }
+        C += sc;
+        put(putb, t & 1, z);
+        if constexpr (!FWD_ONLY) {
+            if (!(a.ablate & 8)) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) ckw[((long long)t * NT * 4 + r) * 64] = z[r];
+            }
+            if (m == 0 && g == 0) ew[t * kTileSeqs] = sc;
+        }
+        if (!(a.ablate & 16)) __syncthreads();
+    };
+    auto forward = [&](auto MASK_) {
+        for (int c = 0; c < nch; ++c) {
+            const uint4 pc = loadpack(c);
+            const uint4 pn = loadpack(c + 1 < nch ? c + 1 : c);
+#pragma unroll
+            for (int k = 0; k < kChunk; ++k) {
+                const int t = c * kChunk + k;
+                bring[(k + 1) & 1] = emis(k + 1 < kChunk ? sym_of(pc, k + 1) : sym_of(pn, 0));  // b(o_{t+1})
+                if (t >= Tw) continue;  // tile-uniform
+                fstep(t, bring[k & 1], MASK_);
+            }
+        }
+    };
+    if (full) forward(std::false_type{});
+    else forward(std::true_type{});
+
+    // log P(O|lambda) = log(sum_j z_{T-1}(j)) + ln2 * C   (:375-377)
+    double ps = (z[0] + z[1]) + (z[2] + z[3]);
+    ps += __shfl_xor(ps, 16);
+    ps += __shfl_xor(ps, 32);
+    if (g == 0) sRed[m * kTileSeqs + s] = ps;
+    __syncthreads();
+    double phat = 0.0;
+#pragma unroll
+    for (int mm = 0; mm < NT; ++mm) phat += sRed[mm * kTileSeqs + s];
+    const bool alive = (T > 0) && (phat > 0.0);
+    const double lp = alive ? (log(phat) + (double)C * 0.69314718055994530942) : -INFINITY;
+    if (m == 0 && g == 0 && T > 0 && seq >= 0) a.logp[seq] = lp;
+    const bool ll_valid = (m == 0) && (g == 0) && (T > 0);
+
+    if constexpr (!FWD_ONLY) if (!(a.ablate & 2)) {
+        // ------------- backward fused with gamma / xi / M-step numerators (:370-410, :474-485) -------------
+        double *accb = a.copies + (long long)(blockIdx.x % a.ncopies) * a.copy_len;
+        const double inv_p = alive ? 1.0 / phat : 0.0;  // beta_hat_{T-1}: folds 1/P (:392, :407)
+        // gamma_{T-1} = z_{T-1} / P (:392 at t = T-1): its gamma row, gamma_den_all, pi_num when T = 1
+        {
+            f64x4 gT;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) gT[r] = z[r] * inv_p;
+            if (T > 0 && !(a.ablate & 4)) putg(T - 1, gT);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int j = 16 * m + g + 4 * r;
+                const double x1 = rowsum(gT[r]), x2 = rowsum(T == 1 ? gT[r] : 0.0);
+                if (s == 0 && j < N) {
+                    if (x1 != 0.0) unsafeAtomicAdd(&accb[a.off_gall + j], x1);
+                    if (x2 != 0.0) unsafeAtomicAdd(&accb[j], x2);  // pi_num at offset 0
+                }
+            }
+        }
+        // backward A operands A[i][j] (i = 16m + (lane&15), j = 4kb + (lane>>4))
+#pragma unroll
+        for (int kb = 0; kb < KB; ++kb) {
+            const int i = 16 * m + (lane & 15), jj = 4 * kb + (lane >> 4);
+            aop[kb] = (i < N && jj < N) ? a.A[i * N + jj] : 0.0;
+        }
+        f64x4 beta = {inv_p, inv_p, inv_p, inv_p};
+        f64x4 gex = {0.0, 0.0, 0.0, 0.0};
+        f64x4 S[NT];
+#pragma unroll
+        for (int mm = 0; mm < NT; ++mm) S[mm] = f64x4{0.0, 0.0, 0.0, 0.0};
+        // ring (slot t % 2, loaded one step ahead): alpha_hat_t, b(o_{t+1}), s_{t+1}
+        f64x4 zring[2], bring1[2];
+        int sring[2];
+        auto ldz = [&](int t) -> f64x4 {
+            f64x4 v;
+            if (a.ablate & 8) return f64x4{0.5, 0.5, 0.5, 0.5};
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = ckw[((long long)t * NT * 4 + r) * 64];
+            return v;
+        };
+        // one regular step t <= Tw - 2 (MASK: per-sequence t <= T - 2 in ragged tiles)
+        auto bstep = [&](int t, const f64x4 &zt, const f64x4 &b1, int s1, auto MASK_) {
+            constexpr bool MASK = decltype(MASK_)::value;
+            const bool reg = !MASK || t <= T - 2;
+            f64x4 v, zs;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                // v_j = b_j(o_{t+1}) 2^{-s_{t+1}} beta_hat_{t+1}(j) (:182-197)
+                v[r] = __builtin_amdgcn_ldexp(b1[r] * beta[r], -s1);
+                if constexpr (MASK) {
+                    v[r] = reg ? v[r] : 0.0;
+                    zs[r] = reg ? zt[r] : 0.0;
+                } else {
+                    zs[r] = zt[r];
+                }
+            }
+            const int p = t & 1;
+            put(putb, p, v);
+            put(putb + 2 * IMG, p, zs);
+            if (!(a.ablate & 16)) __syncthreads();
+            // beta_hat_t = A v (:163-199), this wave's 16 rows
+            const double *vsrc = bopb + p * IMG;
+            f64x4 acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int kb = 0; kb < KB; kb += 2) {
+                acc0 = mfma_f64(aop[kb], vsrc[4 * kb * kXs], acc0);
+                acc1 = mfma_f64(aop[kb + 1], vsrc[4 * (kb + 1) * kXs], acc1);
+            }
+            // S_ij += sum_s z_t(i, s) v_{t+1}(j, s): xi_t(i,j) / a_ij (:396-410)
+            const double *tsrc = topb + p * IMG;
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk) {
+                const double za = tsrc[2 * IMG + 16 * m * kXs + 4 * kk];
+#pragma unroll
+                for (int mj = 0; mj < NT; ++mj) S[mj] = mfma_f64(za, tsrc[16 * mj * kXs + 4 * kk], S[mj]);
+            }
+            f64x4 gm;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const double bn = acc0[r] + acc1[r];
+                gm[r] = zs[r] * bn;  // gamma_t (:392); 0 past the sequence's end
+                if constexpr (MASK) beta[r] = reg ? bn : beta[r];
+                else beta[r] = bn;
+                gex[r] += gm[r];
+            }
+            if ((!MASK || reg) && !(a.ablate & 4)) putg(t, gm);  // B numerator row (:474-485)
+            if (t == 0) {  // pi_num (:415-420): gamma_0 summed over the tile's sequences
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int j = 16 * m + g + 4 * r;
+                    const double x = rowsum(gm[r]);
+                    if (s == 0 && j < N && x != 0.0) unsafeAtomicAdd(&accb[j], x);
+                }
+            }
+        };
+        auto backward = [&](auto MASK_) {
+            zring[1] = f64x4{0.0, 0.0, 0.0, 0.0};
+            bring1[1] = zring[1];
+            sring[1] = 0;
+            for (int c = nch - 1; c >= 0; --c) {
+                const uint4 pc = loadpack(c);
+#pragma unroll
+                for (int k = kChunk - 1; k >= 0; --k) {
+                    const int t = c * kChunk + k;
+                    // step t-1's inputs into the slot step t+1 has consumed
+                    if (t >= 1) {
+                        zring[(k + 1) & 1] = ldz(t - 1);
+                        bring1[(k + 1) & 1] = emis(sym_of(pc, k));  // b(o_t)
+                        sring[(k + 1) & 1] = ew[t * kTileSeqs];     // s_t
+                    }
+                    if (t > Tw - 2) continue;  // tile-uniform; gamma_{T-1} is done above
+                    bstep(t, zring[k & 1], bring1[k & 1], sring[k & 1], MASK_);
+                }
+            }
+        };
+        if (full) backward(std::false_type{});
+        else backward(std::true_type{});
+        // ---- flush: xi = a_ij S_ij; gamma sums reduced over the tile's sequences ----
+#pragma unroll
+        for (int mj = 0; mj < NT; ++mj)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int i = 16 * m + g + 4 * r, jj = 16 * mj + (lane & 15);
+                if (i < N && jj < N && S[mj][r] != 0.0) {
+                    const double x = S[mj][r] * a.A[i * N + jj];
+                    if (x != 0.0) unsafeAtomicAdd(&accb[a.off_S + (long long)i * N + jj], x);
+                }
+            }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const double x0 = rowsum(gex[r]);
+            const int j = 16 * m + g + 4 * r;
+            if (s == 0 && j < N && x0 != 0.0) {
+                unsafeAtomicAdd(&accb[a.off_gex + j], x0);
+                unsafeAtomicAdd(&accb[a.off_gall + j], x0);  // gamma_den_all = excl + the last frames
+            }
+        }
+    }
+    __syncthreads();
+    block_ll_partial(lp, ll_valid, sRed + NT * kTileSeqs, a.llpart + 2 * (long long)blockIdx.x);
+}
+
+// B numerator of the wide kernels (:474-485): B_num[k][j] = sum of the gamma rows of every position
+// whose symbol is k.  One workgroup per symbol; its 4 waves take every 4th position of the symbol's
+// list (rows[ptr[k] .. ptr[k+1]), row indices into the gamma buffer, NP doubles each, bt_col order),
+// lane = column; fixed summation order, plain stores into the symbol-major [K][N] statistics block.
+__global__ void __launch_bounds__(256) k_bnum_gather(const double *gam, const unsigned *rows, const long long *ptr,
+                                                      int NP, int N, double *bnum, const IterState *state) {
+    __shared__ double sh[4][64];
+    if (state != nullptr && state->done) return;
+    const int k = blockIdx.x, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const long long b = ptr[k], e = ptr[k + 1];
+    const int q = lane < NP ? lane : 0;
+    constexpr int U = 8;
+    double acc = 0.0;
+    for (long long p0 = b + wv; p0 < e; p0 += 4 * U) {
+        unsigned rw[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const long long p = p0 + 4 * u;
+            rw[u] = rows[p < e ? p : b];
+        }
+        double x[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) x[u] = gam[(long long)rw[u] * NP + q];
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc += (p0 + 4 * u < e) ? x[u] : 0.0;
+    }
+    sh[wv][lane] = acc;
+    __syncthreads();
+    if (wv == 0 && lane < NP) {
+        const double v = (sh[0][lane] + sh[1][lane]) + (sh[2][lane] + sh[3][lane]);
+        const int j = bt_col(lane);  // bt_col is an involution: column -> state
+        if (j < N) bnum[(long long)k * N + j] = v;
+    }
+}
+
+}  // namespace hmmbw

@@ -1,12 +1,17 @@
-// estep_wide_inst.hip — instantiates the wide (16 < N <= 64) E-step / scorer kernels.
+// estep_wide_inst.hip — instantiates the wide (16 < N <= 64) E-step / scorer kernels (fp64 MFMA,
+// estep_mfma.hpp) for NT = 2, 3, 4 sixteen-state blocks.
+#include "estep_mfma.hpp"
 #include "hmmbw_kernels.hpp"
 
 namespace hmmbw {
 
 Kernels wide_kernels(int NP) {
-    if (NP == 32) return Kernels{k_estep_wide<32, false>, k_estep_wide<32, true>};
-    if (NP == 64) return Kernels{k_estep_wide<64, false>, k_estep_wide<64, true>};
+    if (NP == 32) return Kernels{k_estep_mfma<2, false>, k_estep_mfma<2, true>};
+    if (NP == 48) return Kernels{k_estep_mfma<3, false>, k_estep_mfma<3, true>};
+    if (NP == 64) return Kernels{k_estep_mfma<4, false>, k_estep_mfma<4, true>};
     return Kernels{};
 }
+
+BnumFn bnum_gather_kernel() { return k_bnum_gather; }
 
 }  // namespace hmmbw

@@ -192,6 +192,10 @@ struct hmmbw_ctx {
     long long *d_wsym = nullptr, *d_wckoff = nullptr, *d_wspoff = nullptr;
     int *d_wT = nullptr, *d_wfull = nullptr, *d_slen = nullptr, *d_sseq = nullptr;
     double *d_ck = nullptr, *d_logp = nullptr, *d_llpart = nullptr;  // llpart: [2][nblocks][2]
+    // wide path: gamma rows per position and the symbol -> rows index of k_bnum_gather
+    double *d_gam = nullptr;
+    long long *d_bptr = nullptr;
+    unsigned *d_brows = nullptr;
     uint4 *d_sp = nullptr;
     int *d_ebuf = nullptr;
     bool has_obs = false;
@@ -231,6 +235,7 @@ void free_obs(hmmbw_ctx *c) {
     dfree(c->d_sym); dfree(c->d_wsym); dfree(c->d_wckoff); dfree(c->d_wspoff);
     dfree(c->d_wT); dfree(c->d_wfull); dfree(c->d_slen); dfree(c->d_sseq);
     dfree(c->d_ck); dfree(c->d_sp); dfree(c->d_ebuf); dfree(c->d_logp); dfree(c->d_llpart);
+    dfree(c->d_gam); dfree(c->d_bptr); dfree(c->d_brows);
     c->has_obs = false;
 }
 
@@ -252,6 +257,7 @@ EArgs make_eargs(hmmbw_ctx *c) {
     a.A = c->d_A;
     a.Bt = c->d_Bt;
     a.ckpt = c->d_ck;
+    a.gam = c->d_gam;
     a.spack = c->d_sp;
     a.ebuf = c->d_ebuf;
     a.copies = c->copies(0);
@@ -294,6 +300,7 @@ MArgs make_margs(hmmbw_ctx *c, const hmmbw_ctx::Pending &p) {
     m.G = c->G;
     m.world = c->world;
     m.local_lse = p.local ? 1 : 0;
+    m.bt_perm = c->wide ? 1 : 0;
     m.off_S = c->off_S();
     m.off_gex = c->off_gex();
     m.off_gall = c->off_gall();
@@ -318,11 +325,11 @@ int flush_mstep(hmmbw_ctx *c) {
 }
 
 template <class F>
-int launch_lds(F f, unsigned grid, size_t lds, hipStream_t stream, const EArgs &a) {
+int launch_lds(F f, unsigned grid, size_t lds, hipStream_t stream, const EArgs &a, unsigned block = kBlock) {
     if (lds > 64 * 1024)
         HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(f), hipFuncAttributeMaxDynamicSharedMemorySize,
                                     (int)lds));
-    hipLaunchKernelGGL(f, dim3(grid), dim3(kBlock), lds, stream, a);
+    hipLaunchKernelGGL(f, dim3(grid), dim3(block), lds, stream, a);
     HIP_TRY(hipGetLastError());
     return HMMBW_OK;
 }
@@ -338,7 +345,7 @@ int launch_estep(hmmbw_ctx *c, bool fwd_only, const IterState *state, double *co
     a.zero = zero;
     a.zero_len = zero ? zero_len : 0;
     const int wpb = kBlock / kWave;
-    const unsigned grid = (unsigned)((c->nwaves + wpb - 1) / wpb);
+    const unsigned grid = (unsigned)c->nblocks;
     if (grid == 0) return HMMBW_OK;
     bool flip = false;
     if (merge && !fwd_only && c->pend.on && c->can_merge()) {
@@ -361,10 +368,19 @@ int launch_estep(hmmbw_ctx *c, bool fwd_only, const IterState *state, double *co
         HIP_TRY(hipEventRecord(e0, c->stream));
     }
     if (c->wide) {
-        const size_t lds = sizeof(double) * (2 * (size_t)c->NP * 64 + (size_t)wpb * 64 + 8);
+        // [2 or 4][NP][17] exchange images + per-block reduction scratch (estep_mfma.hpp)
+        const int nt = c->NP / 16;
+        const size_t lds = sizeof(double) * ((fwd_only ? 2 * (size_t)c->NP * 17 : 4 * (size_t)c->NP * 17 + (size_t)nt * 4 * nt * 64) +
+                                             (size_t)nt * 16 + 16);
         const Kernels kw = wide_kernels(c->NP);
         KernelFn f = fwd_only ? kw.score : kw.estep;
-        if (int rc = launch_lds(f, grid, lds, c->stream, a)) return rc;
+        if (!f) return fail(HMMBW_E_UNSUPPORTED, "no wide kernel for N");
+        if (int rc = launch_lds(f, grid, lds, c->stream, a, (unsigned)(nt * kWave))) return rc;
+        if (!fwd_only) {  // B numerator: per-symbol gather of the gamma rows (estep_mfma.hpp)
+            hipLaunchKernelGGL(bnum_gather_kernel(), dim3((unsigned)c->K), dim3(256), 0, c->stream, c->d_gam,
+                               c->d_brows, c->d_bptr, c->NP, c->N, a.copies + c->off_bnum(), a.state);
+            HIP_TRY(hipGetLastError());
+        }
     } else {
         const bool lr = c->topo == HMMBW_TOPOLOGY_LEFT_TO_RIGHT;
         const bool lds_tab = c->lds_tables();
@@ -450,9 +466,10 @@ int hmmbw_ctx_create(int device, int n_states, int n_symbols, hmmbw_ctx **out) {
     c->N = n_states;
     c->K = n_symbols;
     c->wide = n_states > 16;
-    c->G = c->wide ? 64 : (n_states <= 2 ? 2 : n_states <= 4 ? 4 : n_states <= 8 ? 8 : 16);
-    c->U = kWave / c->G;
-    c->NP = c->wide ? (n_states <= 32 ? 32 : 64) : 0;
+    // wide: 16-state MFMA blocks, a tile of 16 sequences per workgroup (estep_mfma.hpp)
+    c->NP = c->wide ? 16 * ((n_states + 15) / 16) : 0;
+    c->G = c->wide ? c->NP : (n_states <= 2 ? 2 : n_states <= 4 ? 4 : n_states <= 8 ? 8 : 16);
+    c->U = c->wide ? 16 : kWave / c->G;
     int rc = set_device(c);
     if (!rc) rc = dalloc(&c->d_pi, c->N);
     if (!rc) rc = dalloc(&c->d_A, (size_t)c->N * c->N);
@@ -574,9 +591,9 @@ int hmmbw_set_observations(hmmbw_ctx *c, const int64_t *offsets, const int32_t *
         wck[(size_t)w] = cktot;
         wsp[(size_t)w] = sptot;
         symtot += nch * U * kChunk;
-        if (c->wide) {  // full alpha_hat [t][64] + exponents [t] (+1 chunk)
-            cktot += nch * kChunk * kWave;
-            sptot += nch * kChunk + kChunk;
+        if (c->wide) {  // full alpha_hat [t][NP/16 waves][4][64 lanes] + exponents [t][16]
+            cktot += nch * kChunk * (long long)c->NP * 16;
+            sptot += nch * kChunk * 16;
         } else {        // one checkpoint per chunk [c][64] + exponent packs [c][u]
             cktot += nch * kWave;
             sptot += nch * U;
@@ -599,7 +616,7 @@ int hmmbw_set_observations(hmmbw_ctx *c, const int64_t *offsets, const int32_t *
         }
     free_obs(c);
     const int wpb = kBlock / kWave;
-    const long long nblocks = (nwaves + wpb - 1) / wpb;
+    const long long nblocks = c->wide ? nwaves : (nwaves + wpb - 1) / wpb;  // wide: one tile per block
     int rc = dalloc(&c->d_sym, (size_t)std::max(symtot, 1LL));
     if (!rc) rc = dalloc(&c->d_wsym, (size_t)nwaves);
     if (!rc) rc = dalloc(&c->d_wckoff, (size_t)nwaves);
@@ -613,10 +630,36 @@ int hmmbw_set_observations(hmmbw_ctx *c, const int64_t *offsets, const int32_t *
         if (c->wide) rc = dalloc(&c->d_ebuf, (size_t)std::max(sptot, 1LL));
         else rc = dalloc(&c->d_sp, (size_t)std::max(sptot, 1LL));
     }
+    std::vector<long long> bptr;
+    std::vector<unsigned> brows;
+    if (c->wide) {  // symbol -> gamma-row index (row = tile offset / NP + t * 16 + u), symbol order stable
+        if (cktot / c->NP >= (1LL << 32)) return fail(HMMBW_E_UNSUPPORTED, "too many positions for the wide path");
+        bptr.assign((size_t)c->K + 1, 0);
+        for (int64_t i = 0; i < total; ++i) ++bptr[(size_t)symbols[i] + 1];
+        for (int k = 0; k < c->K; ++k) bptr[(size_t)k + 1] += bptr[(size_t)k];
+        std::vector<long long> fill(bptr.begin(), bptr.end() - 1);
+        brows.resize((size_t)std::max<int64_t>(total, 1));
+        for (long long w = 0; w < nwaves; ++w)
+            for (int u = 0; u < U; ++u) {
+                const long long sl = w * U + u;
+                if (sl >= R) continue;
+                const int64_t r = perm[(size_t)sl];
+                for (int t = 0; t < len[(size_t)r]; ++t)
+                    brows[(size_t)fill[(size_t)symbols[offsets[r] + t]]++] =
+                        (unsigned)(wck[(size_t)w] / c->NP + (long long)t * U + u);
+            }
+        if (!rc) rc = dalloc(&c->d_gam, (size_t)std::max(cktot, 1LL));
+        if (!rc) rc = dalloc(&c->d_bptr, bptr.size());
+        if (!rc) rc = dalloc(&c->d_brows, brows.size());
+    }
     if (!rc) rc = dalloc(&c->d_logp, (size_t)std::max<int64_t>(R, 1));
     if (!rc) rc = dalloc(&c->d_llpart, 4 * (size_t)std::max(nblocks, 1LL));
     if (rc) return rc;
     HIP_TRY(hipMemcpy(c->d_sym, hsym.data(), sizeof(uint16_t) * hsym.size(), hipMemcpyHostToDevice));
+    if (c->wide) {
+        HIP_TRY(hipMemcpy(c->d_bptr, bptr.data(), sizeof(long long) * bptr.size(), hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(c->d_brows, brows.data(), sizeof(unsigned) * brows.size(), hipMemcpyHostToDevice));
+    }
     if (nwaves > 0) {
         HIP_TRY(hipMemcpy(c->d_wsym, wsym.data(), sizeof(long long) * nwaves, hipMemcpyHostToDevice));
         HIP_TRY(hipMemcpy(c->d_wckoff, wck.data(), sizeof(long long) * nwaves, hipMemcpyHostToDevice));
@@ -679,7 +722,7 @@ int hmmbw_set_params(hmmbw_ctx *c, const double *pi, const double *A, const doub
         for (int k = 0; k < K; ++k) {
             const double v = clean(B[(size_t)jj * K + k]);
             hB[(size_t)jj * K + k] = v;
-            hBt[(size_t)k * G + jj] = v;
+            hBt[(size_t)k * G + (c->wide ? bt_col(jj) : jj)] = v;
         }
     HIP_TRY(hipMemcpy(c->d_pi, hpi.data(), sizeof(double) * N, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(c->d_A, hA.data(), sizeof(double) * hA.size(), hipMemcpyHostToDevice));

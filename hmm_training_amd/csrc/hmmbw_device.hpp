@@ -94,6 +94,7 @@ struct MArgs {
     double *hist;
     int N, K, G, world;
     int local_lse;
+    int bt_perm;           // 1: B^T columns in the wide kernels' order (wide_col)
     long long off_S, off_gex, off_gall, off_bnum, off_ll;
 };
 
@@ -103,6 +104,7 @@ struct EArgs {
     const double *A;
     const double *Bt;  // [K][G] + G zero pad
     double *ckpt;      // small: checkpoints | wide: alpha_hat
+    double *gam;       // wide: gamma rows [position][NP] (bt_col order) for k_bnum_gather
     uint4 *spack;      // small: scale exponents
     int *ebuf;         // wide: scale exponents
     double *copies;    // [ncopies][copy_len] statistics accumulators (workgroup b adds into copy b % ncopies)
@@ -760,143 +762,6 @@ __global__ void __launch_bounds__(kBlock) k_estep_small(EArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// Wide E-step / scorer: 16 < N <= 64, one sequence per wavefront, lane = state.
-// ---------------------------------------------------------------------------------------------
-template <int NP, bool FWD_ONLY>
-__global__ void __launch_bounds__(kBlock) k_estep_wide(EArgs a) {
-    extern __shared__ double smem[];
-    if (a.state != nullptr && a.state->done) return;
-    const int N = a.N;
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const int j = lane;
-    double *sA = smem;              // [NP][64]  a_ij at [i][j]
-    double *sAT = smem + NP * 64;   // [NP][64]  a_jk at [k][j]
-    double *sX = smem + 2 * NP * 64 + wv * 64;  // per-wave exchange row
-    for (int idx = tid; idx < NP * 64; idx += blockDim.x) {
-        const int r = idx / 64, c = idx % 64;
-        sA[idx] = (r < N && c < N) ? a.A[r * N + c] : 0.0;
-        sAT[idx] = (r < N && c < N) ? a.A[c * N + r] : 0.0;
-    }
-    __syncthreads();
-    const long long wave = (long long)blockIdx.x * (blockDim.x >> 6) + wv;
-    double *accb = a.copies + (long long)(blockIdx.x % a.ncopies) * a.copy_len;
-    double logp_lane = -INFINITY;
-    bool ll_valid = false;
-    [&]() {
-    if (wave >= a.L.nwaves) return;
-    const int T = a.L.slot_len[wave];
-    const int seq = a.L.slot_seq[wave];
-    if (T <= 0) return;
-    const int nch = (T + kChunk - 1) / kChunk;
-    const uint16_t *symw = a.L.sym + a.L.wave_symoff[wave];
-    double *aw = a.ckpt + (FWD_ONLY ? 0 : a.L.wave_ckoff[wave]) + lane;
-    int *ew = a.ebuf + (FWD_ONLY ? 0 : a.L.wave_spoff[wave]);
-    const bool jv = j < N;
-    const double pij = jv ? a.pi[j] : 0.0;
-    auto loadpack = [&](int c) -> uint4 { return *reinterpret_cast<const uint4 *>(symw + (long long)c * kChunk); };
-    auto xchg = [&](double v) {
-        __builtin_amdgcn_wave_barrier();
-        sX[lane] = v;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    };
-
-    double alpha = 0.0;
-    int E = 0;
-    uint4 pk = loadpack(0);
-    for (int c = 0; c < nch; ++c) {
-        const uint4 pkn = (c + 1 < nch) ? loadpack(c + 1) : pk;
-        for (int s = 0; s < kChunk; ++s) {
-            const int t = c * kChunk + s;
-            if (t >= T) break;
-            const int o = sym_of(pk, s);
-            const double b = a.Bt[(long long)o * 64 + j];
-            double x;
-            if (t == 0) {
-                x = pij * b;
-            } else {
-                xchg(alpha);
-                double acc0 = 0.0, acc1 = 0.0;
-#pragma unroll 8
-                for (int i = 0; i < NP; i += 2) {
-                    acc0 = fma(sX[i], sA[i * 64 + j], acc0);
-                    acc1 = fma(sX[i + 1], sA[(i + 1) * 64 + j], acc1);
-                }
-                x = (acc0 + acc1) * b;
-            }
-            const double sum = gsum<64>(x);
-            const int e = __builtin_amdgcn_frexp_exp(sum);
-            x = pow2_scale(x, e);
-            alpha = x;
-            E += e;
-            if constexpr (!FWD_ONLY) {
-                aw[(long long)t * kWave] = x;
-                if (j == 0) ew[t] = e;
-            }
-        }
-        pk = pkn;
-    }
-    const double phat = gsum<64>(alpha);
-    const bool alive = phat > 0.0;
-    const double lp = alive ? (log(phat) + (double)E * 0.69314718055994530942) : -INFINITY;
-    if (j == 0 && seq >= 0) a.logp[seq] = lp;
-    logp_lane = lp;
-    ll_valid = j == 0;
-    if constexpr (!FWD_ONLY) {
-        if (!alive) return;
-        double S[NP];
-#pragma unroll
-        for (int k = 0; k < NP; ++k) S[k] = 0.0;
-        double gex = 0.0, pin = 0.0;
-        double beta = 1.0 / phat;
-        auto symat = [&](int t) -> int { return symw[(long long)(t / kChunk) * kChunk + (t % kChunk)]; };
-        const double glast = alpha * beta;
-        double gall = glast;
-        if (T == 1) pin = glast;
-        if (jv) unsafeAtomicAdd(&accb[a.off_bnum + (long long)symat(T - 1) * N + j], glast);
-        int o1 = symat(T - 1);
-        for (int t = T - 2; t >= 0; --t) {
-            const int o0 = symat(t);
-            const double at = aw[(long long)t * kWave];
-            const int e1 = ew[t + 1];
-            const double b1 = a.Bt[(long long)o1 * 64 + j];
-            const double v = pow2_scale(b1 * beta, e1);
-            xchg(v);
-            double b0 = 0.0, bb = 0.0;
-#pragma unroll
-            for (int k = 0; k < NP; k += 2) {
-                const double v0 = sX[k], v1 = sX[k + 1];
-                b0 = fma(sAT[k * 64 + j], v0, b0);
-                bb = fma(sAT[(k + 1) * 64 + j], v1, bb);
-                S[k] = fma(at, v0, S[k]);
-                S[k + 1] = fma(at, v1, S[k + 1]);
-            }
-            const double bn = b0 + bb;
-            const double g = at * bn;
-            beta = bn;
-            gex += g;
-            if (t == 0) pin = g;
-            if (jv) unsafeAtomicAdd(&accb[a.off_bnum + (long long)o0 * N + j], g);
-            o1 = o0;
-        }
-        gall += gex;
-        if (jv) {
-#pragma unroll
-            for (int k = 0; k < NP; ++k)
-                if (k < N && S[k] != 0.0)  // xi_t(j,k) = a_jk * S_jk
-                    unsafeAtomicAdd(&accb[a.off_S + (long long)j * N + k], S[k] * sAT[k * 64 + j]);
-            if (gex != 0.0) unsafeAtomicAdd(&accb[a.off_gex + j], gex);
-            if (gall != 0.0) unsafeAtomicAdd(&accb[a.off_gall + j], gall);
-            if (pin != 0.0) unsafeAtomicAdd(&accb[j], pin);
-        }
-    }
-    }();
-    __syncthreads();
-    block_ll_partial(logp_lane, ll_valid, smem + 2 * NP * 64 + 4 * 64, a.llpart + 2 * (long long)blockIdx.x);
-}
-
-// ---------------------------------------------------------------------------------------------
 // Block reductions
 // ---------------------------------------------------------------------------------------------
 __device__ double block_reduce(double x, double *sh, bool is_max) {
@@ -970,6 +835,10 @@ __device__ __forceinline__ double take(const MArgs &m, long long idx) {
 // B entry from its numerator and the reciprocal of its row's denominator (:460-497): 1e-20 floor when
 // no gamma term carries the symbol, 0 for an empty row.  Shared by every M-step variant, so they
 // produce bit-identical parameters.
+// Column of state j in the wide kernels' emission table (estep_mfma.hpp): j = 16m + 4r + g is stored
+// at 16m + 4g + r, so the 4 states one lane owns are contiguous.
+__host__ __device__ inline int bt_col(int j) { return (j & ~15) | ((j & 3) << 2) | ((j >> 2) & 3); }
+
 __device__ __forceinline__ double mstep_inv(double den) { return den > 0.0 ? 1.0 / den : 0.0; }
 __device__ __forceinline__ double bnum_to_b(double num, double inv) {
     return inv > 0.0 ? (num > 0.0 ? num * inv : 1e-20) : 0.0;
@@ -1049,7 +918,7 @@ __device__ void mstep_block(const MArgs &m) {
         const double num = take<ATOMIC>(m, m.off_bnum + idx);
         const double v = bnum_to_b(num, mstep_inv(sGall[jj]));
         m.B[(long long)jj * K + k] = v;
-        m.Bt[(long long)k * m.G + jj] = v;
+        m.Bt[(long long)k * m.G + (m.bt_perm ? bt_col(jj) : jj)] = v;
     }
     __syncthreads();
     if (tid == 0) record_iteration(m, *st, sL);
@@ -1150,7 +1019,7 @@ __device__ void mstep_staged(const MArgs &m, double *sSt) {
         const int k = idx / N, jj = idx - k * N;
         const double v = bnum_to_b(sBn[idx], mstep_inv(sGall[jj]));
         m.B[(long long)jj * K + k] = v;
-        m.Bt[(long long)k * m.G + jj] = v;
+        m.Bt[(long long)k * m.G + (m.bt_perm ? bt_col(jj) : jj)] = v;
     }
     if (tid == 0) record_iteration(m, in, sL);
 }

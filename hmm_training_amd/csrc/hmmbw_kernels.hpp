@@ -21,7 +21,11 @@ struct Kernels {
 template <int N>
 Kernels small_kernels_n(bool lr, bool ldstab);
 
-// Wide kernels (16 < N <= 64) for the padded state count NP (32 or 64).
+// Wide kernels (16 < N <= 64) for the padded state count NP (32, 48 or 64).
 Kernels wide_kernels(int NP);
+
+// The wide path's B-numerator gather (estep_mfma.hpp).
+using BnumFn = void (*)(const double *, const unsigned *, const long long *, int, int, double *, const IterState *);
+BnumFn bnum_gather_kernel();
 
 }  // namespace hmmbw

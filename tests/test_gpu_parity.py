@@ -130,7 +130,8 @@ def random_problem(rng, N, K, R, tmax, topology):
 
 SWEEP = [(N, K, topo) for N in (1, 2, 3, 4, 5, 7, 8, 9, 12, 16) for K, topo in ((16, "dense"), (256, "left_to_right"))]
 SWEEP += [(8, 700, "dense"), (8, 700, "left_to_right"), (16, 300, "dense"), (17, 40, "dense"), (24, 128, "dense"),
-          (33, 64, "dense"), (64, 300, "dense")]
+          (33, 64, "dense"), (40, 96, "dense"), (48, 200, "dense"), (49, 50, "dense"), (64, 300, "dense"),
+          (64, 1024, "dense")]
 
 
 SAFE_SWEEP = [(N, K, topo) for (N, K, topo) in SWEEP if N in (2, 5, 8, 16)]
@@ -274,14 +275,15 @@ def test_score_matrix_and_timing():
         assert n == 4 and ms > 0
 
 
-@pytest.mark.parametrize("topology", ["left_to_right", "dense"])
+@pytest.mark.parametrize("N,topology", [(8, "left_to_right"), (8, "dense"), (40, "dense")])
 @pytest.mark.parametrize("equal_lengths", [True, False])
-def test_pathological_emissions_fall_back_to_safe_scaling(topology, equal_lengths, oracle):
-    """A symbol with probability 1e-200 in every state collapses the lagged scaling; the kernel must
-    detect it and redo the wave with per-step normalisation, matching the log-domain oracle."""
+def test_pathological_emissions_fall_back_to_safe_scaling(N, topology, equal_lengths, oracle):
+    """A symbol with probability 1e-200 in every state collapses the lagged scaling; the small kernel
+    must detect it and redo the wave with per-step normalisation, and the wide (MFMA) kernel's per-step
+    power-of-two normalisation must absorb it, both matching the log-domain oracle."""
     from hmm_training_amd.engine import BaumWelchEngine, to_csr
     rng = np.random.default_rng(99)
-    N, K = 8, 32
+    K = 32
     obs, pi, A, B = random_problem(rng, N, K, R=24, tmax=60, topology=topology)
     if equal_lengths:
         obs = [rng.integers(0, K, size=60) for _ in range(24)]

@@ -5,7 +5,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np, torch
 from hmm_training_amd.engine import BaumWelchEngine
 from hmm_training_amd.hmm_training import default_initial_params
-R, T, N, K = int(os.environ.get("R", 10000)), 200, 8, 256
+R, T, N, K = (int(os.environ.get(k, d)) for k, d in (("R", 10000), ("T", 200), ("N", 8), ("K", 256)))
 rng = np.random.default_rng(3)
 sym = rng.integers(0, K, size=R * T).astype(np.int32)
 off = np.arange(R + 1, dtype=np.int64) * T
