@@ -15,7 +15,9 @@ Prints ONE JSON line (rank 0) with the driver's fields plus:
   roofline     — achieved = algorithmic bytes per E-step launch (B_u = 24T + 16NT + 8
                  per sequence) / the E-step kernel's mean duration from HIP events on its stream;
                  traffic = measured HBM bytes per launch from the committed rocprofv3 PMC summary
-                 (profiles/), or null when none matches this config.
+                 (profiles/), or null when none matches this config.  For N > 16 (the fp64-MFMA wide
+                 path, cfg5) the bound is "mfma": achieved = 8 N^2 T flops per sequence / kernel time
+                 against the 78.6 TFLOP/s dense fp64 matrix peak.
   cpu_baseline — the oracle C restatement (oracle/bw_oracle.c, log domain like the reference) timed on
                  one host core over a bounded sample of the same workload (rank 0, N=1 only).
 """
@@ -34,6 +36,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+FP64_MFMA_PEAK_TFS = 78.6  # MI355X dense fp64 matrix peak (vendor spec)
 
 
 def parse():
@@ -65,6 +68,18 @@ def init_params(N, K, topology, rng):
 
 def bytes_per_sequence(T, N):
     return 24 * T + 16 * N * T + 8
+
+
+def flops_per_sequence(T, N):
+    return 8 * N * N * T  # forward + backward + xi, fp64
+
+
+def workload_name(R, T, N, K):
+    if (T, N, K) == (200, 8, 256):
+        return "cfg3" if R == 10_000 else ("cfg4" if R == 12_500 else "cfg3-shape")
+    if (T, N, K) == (400, 64, 1024):
+        return "cfg5" if R == 6_250 else "cfg5-shape"
+    return "custom"
 
 
 def find_traffic(cfg_key):
@@ -162,13 +177,28 @@ def main():
     value = R * world * args.steps / elapsed
     kern_s = kern_ms / max(kern_n, 1) / 1000.0
     bu = bytes_per_sequence(T, N)
-    achieved = bu * R / kern_s / 1e9 if kern_s > 0 else float("nan")
+    wide = N > 16
     cfg_key = f"R{R}_T{T}_N{N}_K{K}_{args.topology}"
     traffic = find_traffic(cfg_key)
+    if wide:  # fp64 MFMA recursions (estep_mfma.hpp): priced against the dense fp64 matrix peak
+        achieved = flops_per_sequence(T, N) * R / kern_s / 1e12 if kern_s > 0 else float("nan")
+        roof = {"bound": "mfma", "achieved": achieved, "peak": FP64_MFMA_PEAK_TFS, "unit": "TFLOP/s",
+                "frac": achieved / FP64_MFMA_PEAK_TFS, "traffic": traffic[0] if traffic else None,
+                "kernel": "k_estep_mfma + k_bnum_gather (E-step)", "kernel_ms": kern_s * 1000.0,
+                "flops_per_launch_algorithmic": flops_per_sequence(T, N) * R,
+                "traffic_source": traffic[1] if traffic else None}
+    else:
+        achieved = bu * R / kern_s / 1e9 if kern_s > 0 else float("nan")
+        roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS, "traffic": traffic[0] if traffic else None,
+                "kernel": "k_estep_small (E-step)", "kernel_ms": kern_s * 1000.0,
+                "bytes_per_launch_algorithmic": bu * R,
+                "traffic_source": traffic[1] if traffic else None}
+    wl = workload_name(R, T, N, K)
 
     if rank == 0:
         out = {
-            "metric": "Baum-Welch utterances/sec/iter (T=200,N=8,K=256)",
+            "metric": f"Baum-Welch utterances/sec/iter (T={T},N={N},K={K})",
             "value": value,
             "unit": "utterances/s/iter",
             "n_gpus": world,
@@ -180,16 +210,11 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (uniform random symbols, seeded); reference-topology random init",
-            "config": {"workload": f"cfg3 per GPU: R={R} sequences x T={T}, N={N} states, K={K} symbols, "
+            "config": {"workload": f"{wl} per GPU: R={R} sequences x T={T}, N={N} states, K={K} symbols, "
                                    f"{args.topology} A, one EM iteration per step",
                        "sequences_per_gpu": R, "T": T, "N": N, "K": K, "topology": args.topology,
                        "parallelism": f"dp{world}" if world > 1 else "single"},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": traffic[0] if traffic else None,
-                         "kernel": "k_estep_small (E-step)", "kernel_ms": kern_s * 1000.0,
-                         "bytes_per_launch_algorithmic": bu * R,
-                         "traffic_source": traffic[1] if traffic else None},
+            "roofline": roof,
             "loglik_last": st.last_log_likelihood,
         }
         if world == 1 and not args.no_cpu_baseline:

@@ -13,10 +13,14 @@ Kernels small_kernels_n<HMMBW_INST_N>(bool lr, bool ldstab) {
     constexpr int N = HMMBW_INST_N;
     constexpr int G = N <= 2 ? 2 : (N <= 4 ? 4 : (N <= 8 ? 8 : 16));
     if (lr) {
-        if (ldstab) return Kernels{k_estep_small<N, G, true, true, false>, k_estep_small<N, G, true, true, true>};
+        if (ldstab)
+            return Kernels{k_estep_small<N, G, true, true, false>, k_estep_small<N, G, true, true, true>,
+                           k_estep_small_group<N, G, true, true, false>, k_estep_small_group<N, G, true, true, true>};
         return Kernels{k_estep_small<N, G, true, false, false>, k_estep_small<N, G, true, false, true>};
     }
-    if (ldstab) return Kernels{k_estep_small<N, G, false, true, false>, k_estep_small<N, G, false, true, true>};
+    if (ldstab)
+        return Kernels{k_estep_small<N, G, false, true, false>, k_estep_small<N, G, false, true, true>,
+                       k_estep_small_group<N, G, false, true, false>, k_estep_small_group<N, G, false, true, true>};
     return Kernels{k_estep_small<N, G, false, false, false>, k_estep_small<N, G, false, false, true>};
 }
 

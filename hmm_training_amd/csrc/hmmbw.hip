@@ -334,26 +334,70 @@ int launch_lds(F f, unsigned grid, size_t lds, hipStream_t stream, const EArgs &
     return HMMBW_OK;
 }
 
+// One E-step / scorer launch of a context, resolved but not yet enqueued (launch_estep enqueues it
+// alone, group_launch concatenates several contexts' plans into one grouped launch).
+struct Plan {
+    EArgs a{};
+    KernelFn fn = nullptr;
+    GroupFn gfn = nullptr;
+    unsigned grid = 0, block = kBlock;
+    size_t lds = 0;
+    bool flip = false;
+};
+
 // E-step launch e accumulates into copies and llpart; it clears `zero` (zero_len doubles) and, when
 // `merge` is set, first runs the pending M-step in its prologue (which consumes c->pend).
-int launch_estep(hmmbw_ctx *c, bool fwd_only, const IterState *state, double *copies = nullptr,
-                 double *llpart = nullptr, double *zero = nullptr, long long zero_len = 0, bool merge = false) {
-    EArgs a = make_eargs(c);
+int plan_estep(hmmbw_ctx *c, bool fwd_only, const IterState *state, double *copies, double *llpart, double *zero,
+               long long zero_len, bool merge, Plan *P) {
+    Plan &p = *P;
+    p = Plan{};
+    EArgs &a = p.a;
+    a = make_eargs(c);
     a.state = state;
     if (copies) a.copies = copies;
     if (llpart) a.llpart = llpart;
     a.zero = zero;
     a.zero_len = zero ? zero_len : 0;
     const int wpb = kBlock / kWave;
-    const unsigned grid = (unsigned)c->nblocks;
-    if (grid == 0) return HMMBW_OK;
-    bool flip = false;
-    if (merge && !fwd_only && c->pend.on && c->can_merge()) {
+    p.grid = (unsigned)c->nblocks;
+    if (c->wide) {
+        // [2 or 4][NP][17] exchange images + per-block reduction scratch (estep_mfma.hpp)
+        const int nt = c->NP / 16;
+        p.lds = sizeof(double) * ((fwd_only ? 2 * (size_t)c->NP * 17 : 4 * (size_t)c->NP * 17 + (size_t)nt * 4 * nt * 64) +
+                                  (size_t)nt * 16 + 16);
+        const Kernels kw = wide_kernels(c->NP);
+        p.fn = fwd_only ? kw.score : kw.estep;
+        p.block = (unsigned)(nt * kWave);
+        if (!p.fn) return fail(HMMBW_E_UNSUPPORTED, "no wide kernel for N");
+    } else {
+        const bool lr = c->topo == HMMBW_TOPOLOGY_LEFT_TO_RIGHT;
+        const bool lds_tab = c->lds_tables();
+        Kernels ks = lr ? (lds_tab ? pick_small_n<true, true>(c->N) : pick_small_n<true, false>(c->N))
+                        : (lds_tab ? pick_small_n<false, true>(c->N) : pick_small_n<false, false>(c->N));
+        p.fn = fwd_only ? ks.score : ks.estep;
+        p.gfn = fwd_only ? ks.group_score : ks.group_estep;
+        if (!p.fn) return fail(HMMBW_E_UNSUPPORTED, "no kernel for N");
+        const int NV = (lr ? 2 : c->N) + 3;
+        const size_t GP = (size_t)c->G + 1;
+        const size_t ntab = ((((size_t)c->K + 1) * GP) + 1) & ~(size_t)1;
+        const size_t tabs = lds_tab ? ntab * (lr ? 3 : 1) + (fwd_only ? 0 : (size_t)c->K * GP) : 0;
+        p.lds = sizeof(double) * (tabs + (size_t)wpb * c->G * NV + 8);
+    }
+    if (p.grid > 0 && merge && !fwd_only && c->pend.on && c->can_merge()) {
         a.merged = 1;
         a.m = make_margs(c, c->pend);
         c->pend.on = false;
-        flip = true;  // the launch's M-step writes the other state slot
+        p.flip = true;  // the launch's M-step writes the other state slot
     }
+    return HMMBW_OK;
+}
+
+int launch_estep(hmmbw_ctx *c, bool fwd_only, const IterState *state, double *copies = nullptr,
+                 double *llpart = nullptr, double *zero = nullptr, long long zero_len = 0, bool merge = false) {
+    Plan p;
+    if (int rc = plan_estep(c, fwd_only, state, copies, llpart, zero, zero_len, merge, &p)) return rc;
+    if (p.grid == 0) return HMMBW_OK;
+    const EArgs &a = p.a;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (c->timing && !fwd_only && (c->timing_seq++ % c->timing) == 0) {
         if (c->ev_free.size() < 2) {
@@ -367,35 +411,13 @@ int launch_estep(hmmbw_ctx *c, bool fwd_only, const IterState *state, double *co
         e0 = c->ev_free.back(); c->ev_free.pop_back();
         HIP_TRY(hipEventRecord(e0, c->stream));
     }
-    if (c->wide) {
-        // [2 or 4][NP][17] exchange images + per-block reduction scratch (estep_mfma.hpp)
-        const int nt = c->NP / 16;
-        const size_t lds = sizeof(double) * ((fwd_only ? 2 * (size_t)c->NP * 17 : 4 * (size_t)c->NP * 17 + (size_t)nt * 4 * nt * 64) +
-                                             (size_t)nt * 16 + 16);
-        const Kernels kw = wide_kernels(c->NP);
-        KernelFn f = fwd_only ? kw.score : kw.estep;
-        if (!f) return fail(HMMBW_E_UNSUPPORTED, "no wide kernel for N");
-        if (int rc = launch_lds(f, grid, lds, c->stream, a, (unsigned)(nt * kWave))) return rc;
-        if (!fwd_only) {  // B numerator: per-symbol gather of the gamma rows (estep_mfma.hpp)
-            hipLaunchKernelGGL(bnum_gather_kernel(), dim3((unsigned)c->K), dim3(256), 0, c->stream, c->d_gam,
-                               c->d_brows, c->d_bptr, c->NP, c->N, a.copies + c->off_bnum(), a.state);
-            HIP_TRY(hipGetLastError());
-        }
-    } else {
-        const bool lr = c->topo == HMMBW_TOPOLOGY_LEFT_TO_RIGHT;
-        const bool lds_tab = c->lds_tables();
-        Kernels ks = lr ? (lds_tab ? pick_small_n<true, true>(c->N) : pick_small_n<true, false>(c->N))
-                        : (lds_tab ? pick_small_n<false, true>(c->N) : pick_small_n<false, false>(c->N));
-        KernelFn f = fwd_only ? ks.score : ks.estep;
-        if (!f) return fail(HMMBW_E_UNSUPPORTED, "no kernel for N");
-        const int NV = (lr ? 2 : c->N) + 3;
-        const size_t GP = (size_t)c->G + 1;
-        const size_t ntab = ((((size_t)c->K + 1) * GP) + 1) & ~(size_t)1;
-        const size_t tabs = lds_tab ? ntab * (lr ? 3 : 1) + (fwd_only ? 0 : (size_t)c->K * GP) : 0;
-        size_t lds = sizeof(double) * (tabs + (size_t)wpb * c->G * NV + 8);
-        if (int rc = launch_lds(f, grid, lds, c->stream, a)) return rc;
+    if (int rc = launch_lds(p.fn, p.grid, p.lds, c->stream, a, p.block)) return rc;
+    if (c->wide && !fwd_only) {  // B numerator: per-symbol gather of the gamma rows (estep_mfma.hpp)
+        hipLaunchKernelGGL(bnum_gather_kernel(), dim3((unsigned)c->K), dim3(256), 0, c->stream, c->d_gam,
+                           c->d_brows, c->d_bptr, c->NP, c->N, a.copies + c->off_bnum(), a.state);
+        HIP_TRY(hipGetLastError());
     }
-    if (flip) c->scur ^= 1;
+    if (p.flip) c->scur ^= 1;
     if (e1) {
         HIP_TRY(hipEventRecord(e1, c->stream));
         c->ev_pending.push_back(e0);
@@ -896,5 +918,257 @@ int hmmbw_timing(hmmbw_ctx *c, int enable, double *total_ms, int64_t *count) {
     return HMMBW_OK;
 }
 
+
+
+// ---------------------------------------------------------------------------------------------
+// Groups: several single-rank contexts of one shape advanced by ONE grouped launch per EM iteration
+// (k_estep_small_group).  The reference trains its word models one after another (HMM/main.py:147-152
+// -> training_with_save, hmm_training.py:215-247) and scores every (recording, model) pair with its
+// own forward pass (hmm_testing.py:139-161); a group does each in one launch.
+// ---------------------------------------------------------------------------------------------
+}  // extern "C"
+
+struct hmmbw_group {
+    std::vector<hmmbw_ctx *> m;
+    // argument slabs ([n_launch][n] EArgs + [n_launch][n + 1] first-workgroup tables): pinned staging,
+    // device copy, and the event after the last launch that reads it; reused round-robin
+    struct Slab {
+        char *host = nullptr, *dev = nullptr;
+        size_t cap = 0;
+        hipEvent_t ev = nullptr;
+    };
+    std::vector<Slab> slabs;
+    size_t next = 0;
+    std::vector<hipEvent_t> ev_free, ev_pending;  // timing pairs (start, stop)
+    int timing = 0;
+    double timed_ms = 0.0;
+    long long timed_n = 0, timing_seq = 0;
+};
+
+namespace {
+
+int group_check(hmmbw_group *g, bool need_armed) {
+    if (!g || g->m.empty()) return fail(HMMBW_E_INVALID, "null or empty group");
+    hmmbw_ctx *c0 = g->m[0];
+    for (hmmbw_ctx *c : g->m) {
+        if (int rc = check_ready(c, need_armed)) return rc;
+        if (c->world != 1) return fail(HMMBW_E_STATE, "group members are single-rank contexts");
+        if (c->device != c0->device || c->stream != c0->stream)
+            return fail(HMMBW_E_INVALID, "group members must share the device and the stream");
+        if (c->N != c0->N || c->K != c0->K || c->topo != c0->topo || c->wide || !c->lds_tables())
+            return fail(HMMBW_E_UNSUPPORTED, "group members must share N, M and topology (small-N path with LDS tables)");
+    }
+    return HMMBW_OK;
+}
+
+// Enqueue n_launch grouped launches; plans[l * n + i] is member i's plan for launch l.
+int group_launch(hmmbw_group *g, const std::vector<Plan> &plans, int n_launch, bool timed) {
+    const int n = (int)g->m.size();
+    hipStream_t st = g->m[0]->stream;
+    const size_t args_b = sizeof(EArgs) * (size_t)n, start_b = sizeof(long long) * (size_t)(n + 1);
+    const size_t per = (args_b + start_b + 255) & ~(size_t)255;
+    const size_t need = per * (size_t)n_launch;
+    if (g->slabs.size() < 4) g->slabs.resize(4);
+    hmmbw_group::Slab &sl = g->slabs[g->next];
+    g->next = (g->next + 1) % g->slabs.size();
+    if (sl.ev) HIP_TRY(hipEventSynchronize(sl.ev));  // its previous launches have read it
+    else HIP_TRY(hipEventCreateWithFlags(&sl.ev, hipEventDisableTiming));
+    if (sl.cap < need) {
+        if (sl.host) HIP_TRY(hipHostFree(sl.host));
+        if (sl.dev) HIP_TRY(hipFree(sl.dev));
+        sl.host = sl.dev = nullptr;
+        sl.cap = 0;
+        HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&sl.host), need));
+        HIP_TRY(hipMalloc(reinterpret_cast<void **>(&sl.dev), need));
+        sl.cap = need;
+    }
+    std::vector<unsigned> grid((size_t)n_launch, 0);
+    size_t lds = 0;
+    for (int l = 0; l < n_launch; ++l) {
+        EArgs *A = reinterpret_cast<EArgs *>(sl.host + per * l);
+        long long *S = reinterpret_cast<long long *>(sl.host + per * l + args_b);
+        long long b = 0;
+        for (int i = 0; i < n; ++i) {
+            const Plan &p = plans[(size_t)l * n + i];
+            A[i] = p.a;
+            S[i] = b;
+            b += p.grid;
+            lds = std::max(lds, p.lds);
+        }
+        S[n] = b;
+        grid[(size_t)l] = (unsigned)b;
+    }
+    HIP_TRY(hipMemcpyAsync(sl.dev, sl.host, need, hipMemcpyHostToDevice, st));
+    const GroupFn f = plans[0].gfn;
+    if (lds > 64 * 1024)
+        HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(f), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)lds));
+    for (int l = 0; l < n_launch; ++l) {
+        if (grid[(size_t)l] == 0) continue;
+        GroupArgs ga{reinterpret_cast<const EArgs *>(sl.dev + per * l),
+                     reinterpret_cast<const long long *>(sl.dev + per * l + args_b), n};
+        const bool t = timed && g->timing && (g->timing_seq++ % g->timing) == 0;
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+        if (t) {
+            while (g->ev_free.size() < 2) {
+                hipEvent_t x;
+                HIP_TRY(hipEventCreate(&x));
+                g->ev_free.push_back(x);
+            }
+            e1 = g->ev_free.back(); g->ev_free.pop_back();
+            e0 = g->ev_free.back(); g->ev_free.pop_back();
+            HIP_TRY(hipEventRecord(e0, st));
+        }
+        hipLaunchKernelGGL(f, dim3(grid[(size_t)l]), dim3(kBlock), lds, st, ga);
+        HIP_TRY(hipGetLastError());
+        if (t) {
+            HIP_TRY(hipEventRecord(e1, st));
+            g->ev_pending.push_back(e0);
+            g->ev_pending.push_back(e1);
+        }
+    }
+    HIP_TRY(hipEventRecord(sl.ev, st));
+    return HMMBW_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int hmmbw_group_create(hmmbw_ctx *const *ctxs, int n, hmmbw_group **out) {
+    if (!out || (!ctxs && n > 0)) return fail(HMMBW_E_INVALID, "null argument");
+    if (n <= 0) return fail(HMMBW_E_INVALID, "a group needs at least one context");
+    *out = nullptr;
+    for (int i = 0; i < n; ++i) {
+        if (!ctxs[i]) return fail(HMMBW_E_INVALID, "null context in group");
+        for (int k = 0; k < i; ++k)
+            if (ctxs[k] == ctxs[i]) return fail(HMMBW_E_INVALID, "a context appears twice in the group");
+    }
+    hmmbw_group *g = new hmmbw_group();
+    g->m.assign(ctxs, ctxs + n);
+    if (int rc = group_check(g, false)) {  // members must be set up and of one groupable shape
+        delete g;
+        return rc;
+    }
+    *out = g;
+    return HMMBW_OK;
+}
+
+int hmmbw_group_destroy(hmmbw_group *g) {
+    if (!g) return HMMBW_OK;
+    if (!g->m.empty()) (void)hipSetDevice(g->m[0]->device);
+    for (auto &sl : g->slabs) {
+        if (sl.ev) {
+            (void)hipEventSynchronize(sl.ev);
+            (void)hipEventDestroy(sl.ev);
+        }
+        if (sl.host) (void)hipHostFree(sl.host);
+        if (sl.dev) (void)hipFree(sl.dev);
+    }
+    for (hipEvent_t e : g->ev_free) (void)hipEventDestroy(e);
+    for (hipEvent_t e : g->ev_pending) (void)hipEventDestroy(e);
+    delete g;
+    return HMMBW_OK;
+}
+
+int hmmbw_group_iterate(hmmbw_group *g, int64_t n_iter) {
+    if (int rc = group_check(g, true)) return rc;
+    if (n_iter <= 0) return HMMBW_OK;
+    const int n = (int)g->m.size();
+    constexpr int64_t kBatch = 64;  // launches per argument slab
+    std::vector<Plan> plans;
+    for (int64_t i0 = 0; i0 < n_iter; i0 += kBatch) {
+        const int nl = (int)std::min<int64_t>(kBatch, n_iter - i0);
+        plans.assign((size_t)nl * n, Plan{});
+        // Members whose M-step cannot run in the E-step prologue need their own M-step kernel
+        // between two grouped launches; then the batch is one launch at a time.
+        bool all_merge = true;
+        for (hmmbw_ctx *c : g->m) all_merge = all_merge && c->can_merge();
+        const int step = all_merge ? nl : 1;
+        for (int l0 = 0; l0 < nl; l0 += step) {
+            for (int l = l0; l < l0 + step; ++l)
+                for (int i = 0; i < n; ++i) {
+                    hmmbw_ctx *c = g->m[(size_t)i];
+                    if (c->pend.on && !c->can_merge())
+                        if (int rc = flush_mstep(c)) return rc;
+                    const long long e = c->e_count++;
+                    const long long nz = (long long)c->ncopies * c->copy_len();
+                    Plan &p = plans[(size_t)l * n + i];
+                    if (int rc = plan_estep(c, false, c->state(), c->copies(e), c->llpart(e), c->copies(e + 1), nz,
+                                            true, &p))
+                        return rc;
+                    if (!p.gfn || p.gfn != plans[0].gfn || p.block != kBlock)
+                        return fail(HMMBW_E_UNSUPPORTED, "group members need the same grouped kernel");
+                    if (p.flip) c->scur ^= 1;  // slots are read by the launch through the plan's pointers
+                    hmmbw_ctx::Pending &q = c->pend;
+                    q.on = true;
+                    q.local = true;
+                    q.src = c->copies(e);
+                    q.nsrc = c->ncopies;
+                    q.ll = c->llpart(e);
+                    q.nll = c->nblocks;
+                    q.ext = nullptr;
+                    q.R = c->R;
+                }
+            if (step == nl) {
+                if (int rc = group_launch(g, plans, nl, true)) return rc;
+            } else {
+                std::vector<Plan> one(plans.begin() + (size_t)l0 * n, plans.begin() + (size_t)(l0 + 1) * n);
+                if (int rc = group_launch(g, one, 1, true)) return rc;
+                for (hmmbw_ctx *c : g->m)
+                    if (!c->can_merge())
+                        if (int rc = flush_mstep(c)) return rc;
+            }
+        }
+    }
+    return HMMBW_OK;
+}
+
+int hmmbw_group_score(hmmbw_group *g, double *out) {
+    if (int rc = group_check(g, false)) return rc;
+    if (!out) return fail(HMMBW_E_INVALID, "null argument");
+    const int n = (int)g->m.size();
+    std::vector<Plan> plans((size_t)n);
+    for (int i = 0; i < n; ++i) {
+        hmmbw_ctx *c = g->m[(size_t)i];
+        if (int rc = flush_mstep(c)) return rc;
+        if (int rc = plan_estep(c, true, nullptr, nullptr, nullptr, nullptr, 0, false, &plans[(size_t)i])) return rc;
+        if (!plans[(size_t)i].gfn || plans[(size_t)i].gfn != plans[0].gfn)
+            return fail(HMMBW_E_UNSUPPORTED, "group members need the same grouped kernel");
+    }
+    if (int rc = group_launch(g, plans, 1, false)) return rc;
+    long long off = 0;
+    for (hmmbw_ctx *c : g->m) {
+        if (c->R > 0)
+            HIP_TRY(hipMemcpyAsync(out + off, c->d_logp, sizeof(double) * c->R, hipMemcpyDeviceToHost, c->stream));
+        off += c->R;
+    }
+    HIP_TRY(hipStreamSynchronize(g->m[0]->stream));
+    return HMMBW_OK;
+}
+
+int hmmbw_group_timing(hmmbw_group *g, int enable, double *total_ms, int64_t *count) {
+    if (!g || g->m.empty()) return fail(HMMBW_E_INVALID, "null or empty group");
+    if (int rc = set_device(g->m[0])) return rc;
+    for (size_t i = 0; i + 1 < g->ev_pending.size(); i += 2) {
+        HIP_TRY(hipEventSynchronize(g->ev_pending[i + 1]));
+        float ms = 0.f;
+        HIP_TRY(hipEventElapsedTime(&ms, g->ev_pending[i], g->ev_pending[i + 1]));
+        g->timed_ms += ms;
+        g->timed_n += 1;
+        g->ev_free.push_back(g->ev_pending[i]);
+        g->ev_free.push_back(g->ev_pending[i + 1]);
+    }
+    g->ev_pending.clear();
+    if (total_ms) *total_ms = g->timed_ms;
+    if (count) *count = g->timed_n;
+    if (enable >= 0) {
+        g->timing = enable;
+        g->timing_seq = 0;
+        g->timed_ms = 0.0;
+        g->timed_n = 0;
+    }
+    return HMMBW_OK;
+}
 
 }  // extern "C"

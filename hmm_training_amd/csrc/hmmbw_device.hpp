@@ -124,6 +124,13 @@ struct EArgs {
     long long off_S, off_gex, off_gall, off_bnum;
 };
 
+// Grouped launch (k_estep_small_group): per-model arguments and first workgroups (start[nm] = grid)
+struct GroupArgs {
+    const EArgs *__restrict__ args;
+    const long long *__restrict__ start;
+    int nm;
+};
+
 // ---------------------------------------------------------------------------------------------
 // Cross-lane helpers (DPP on gfx950; 64-bit operands are split or use v_mov_b64_dpp)
 // ---------------------------------------------------------------------------------------------
@@ -258,10 +265,13 @@ __device__ void block_ll_partial(double lp, bool valid, double *sh, double *out)
 // gamma is scattered into the per-workgroup LDS histogram B_num[o_t][j] (ds_add_f64).
 // ---------------------------------------------------------------------------------------------
 template <int N, int G, int GP, bool HIST, bool PT>
-__device__ bool merged_mstep(const EArgs &a, double *sBt, double2 *sBP, double *sBn, double *sPA);
+__device__ bool merged_mstep(const EArgs &a, double *sBt, double2 *sBP, double *sBn, double *sPA, long long bid);
 
+// Body of the small-N E-step / scorer for workgroup `bid` of the `nblk` workgroups that cover one
+// model's sequences: the whole grid of k_estep_small, or one model's slice of a grouped launch
+// (k_estep_small_group, several models of the same shape in one launch).
 template <int N, int G, bool LR, bool LDSTAB, bool FWD_ONLY>
-__global__ void __launch_bounds__(kBlock) k_estep_small(EArgs a) {
+__device__ __forceinline__ void estep_small_body(const EArgs &a, const long long bid, const long long nblk) {
     constexpr int U = kWave / G;
     constexpr int NS = LR ? 2 : N;      // per-lane S accumulators (row j of S)
     constexpr int NV = NS + 3;          // + gamma_den_excl, gamma_den_all, pi_num
@@ -273,8 +283,7 @@ __global__ void __launch_bounds__(kBlock) k_estep_small(EArgs a) {
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     PHASE(0);
     if constexpr (!FWD_ONLY)  // clear the next iteration's statistics (single rank: triple buffer)
-        for (long long i = (long long)blockIdx.x * blockDim.x + tid; i < a.zero_len;
-             i += (long long)gridDim.x * blockDim.x)
+        for (long long i = bid * blockDim.x + tid; i < a.zero_len; i += nblk * blockDim.x)
             a.zero[i] = 0.0;
     const int j = lane & (G - 1), u = lane / G;
     const int K = a.K;
@@ -289,7 +298,7 @@ __global__ void __launch_bounds__(kBlock) k_estep_small(EArgs a) {
         // the previous iteration's M-step, computed redundantly by every workgroup straight into
         // its LDS tables (no separate M-step kernel, no parameter round trip through HBM)
         if constexpr (LDSTAB && !FWD_ONLY)
-            if (!merged_mstep<N, G, GP, true, PT>(a, sBt, sBP, sBn, sPA)) return;  // done or stopped (:346)
+            if (!merged_mstep<N, G, GP, true, PT>(a, sBt, sBP, sBn, sPA, bid)) return;  // done or stopped (:346)
     } else {
         if (a.state != nullptr && a.state->done) return;  // converged: device-side no-op
         if (tid < G) sPA[tid] = tid < N ? a.pi[tid] : 0.0;
@@ -334,8 +343,8 @@ __global__ void __launch_bounds__(kBlock) k_estep_small(EArgs a) {
     const double *Btab = LDSTAB ? sBt : a.Bt;
     PHASE(1);
 
-    const long long wave = (long long)blockIdx.x * (blockDim.x >> 6) + wv;
-    double *accb = a.copies + (long long)(blockIdx.x % a.ncopies) * a.copy_len;
+    const long long wave = bid * (blockDim.x >> 6) + wv;
+    double *accb = a.copies + (bid % a.ncopies) * a.copy_len;
     double S[NS];
 #pragma unroll
     for (int k = 0; k < NS; ++k) S[k] = 0.0;
@@ -705,7 +714,7 @@ __global__ void __launch_bounds__(kBlock) k_estep_small(EArgs a) {
 
     // per-block (max, sum exp) of log P for the convergence scalar
     __syncthreads();
-    block_ll_partial(logp_lane, ll_valid, sRed, a.llpart + 2 * (long long)blockIdx.x);
+    block_ll_partial(logp_lane, ll_valid, sRed, a.llpart + 2 * bid);
     PHASE(4);
 
     if constexpr (!FWD_ONLY) if (!(a.ablate & 1)) {
@@ -759,6 +768,28 @@ __global__ void __launch_bounds__(kBlock) k_estep_small(EArgs a) {
         }
     }
     PHASE(5);
+}
+
+template <int N, int G, bool LR, bool LDSTAB, bool FWD_ONLY>
+__global__ void __launch_bounds__(kBlock) k_estep_small(EArgs a) {
+    estep_small_body<N, G, LR, LDSTAB, FWD_ONLY>(a, blockIdx.x, gridDim.x);
+}
+
+// Grouped launch: g.nm models of one shape (same N, topology and tables), model m owning workgroups
+// [start[m], start[m+1]) with its own arguments args[m] (observations, parameters, statistics,
+// convergence state).  Replaces the per-word loop of HMM/main.py:147-152 (train) and the per-model
+// loop of HMM/hmm_testing.py:139-161 (test) with one launch per EM iteration / per scoring pass.
+template <int N, int G, bool LR, bool LDSTAB, bool FWD_ONLY>
+__global__ void __launch_bounds__(kBlock) k_estep_small_group(GroupArgs g) {
+    const long long b = blockIdx.x;
+    int lo = 0, hi = g.nm - 1;  // the last model whose first workgroup is <= b (uniform search)
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (g.start[mid] <= b) lo = mid;
+        else hi = mid - 1;
+    }
+    const long long b0 = g.start[lo];
+    estep_small_body<N, G, LR, LDSTAB, FWD_ONLY>(g.args[lo], b - b0, g.start[lo + 1] - b0);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1042,7 +1073,7 @@ __device__ __forceinline__ double wave_max(double x) {
 }
 
 template <int N, int G, int GP, bool HIST, bool PT>
-__device__ bool merged_mstep(const EArgs &a, double *sBt, double2 *sBP, double *sBn, double *sPA) {
+__device__ bool merged_mstep(const EArgs &a, double *sBt, double2 *sBP, double *sBn, double *sPA, long long bid) {
     constexpr int NSM = N + N * N + 2 * N;  // pi_num, xi, gamma_den_excl, gamma_den_all
     constexpr int NW = kBlock / 64;
     constexpr int SB = kMergedMaxStats / kBlock;
@@ -1111,7 +1142,7 @@ __device__ bool merged_mstep(const EArgs &a, double *sBt, double2 *sBP, double *
     __syncthreads();
     PHASE(6);
     if (sIn.done) {  // converged before this launch: device-side no-op
-        if (tid == 0 && blockIdx.x == 0) *m.state_out = sIn;
+        if (tid == 0 && bid == 0) *m.state_out = sIn;
         return false;
     }
     double Mb = sMx[0];
@@ -1140,7 +1171,7 @@ __device__ bool merged_mstep(const EArgs &a, double *sBt, double2 *sBP, double *
     // B (:460-497) from the registers straight into the emission table (and HBM, workgroup 0).
     // Element e = q * kBlock + tid - NSM is symbol e / N, state e % N; with N | kBlock the state (and
     // so the denominator) is the same for every q of a thread: one reciprocal per thread.
-    const bool w0 = blockIdx.x == 0;
+    const bool w0 = bid == 0;
     const int e0 = tid - NSM;
     constexpr bool kSameState = (kBlock % N) == 0;
     const int jj0 = ((e0 % N) + N) % N;

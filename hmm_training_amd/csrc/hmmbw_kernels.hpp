@@ -1,7 +1,8 @@
 // hmmbw_kernels.hpp — E-step kernel entry points exported by the instantiation units.
 //
 // The small-N kernel k_estep_small<N, G, LR, LDSTAB, FWD_ONLY> has 128 instantiations (N = 1..16 x
-// topology x LDS tables x E-step/scorer); each N lives in its own translation unit
+// topology x LDS tables x E-step/scorer), plus 64 of the grouped form k_estep_small_group (LDS tables
+// only); each N lives in its own translation unit
 // (estep_small_inst.hip compiled with -DHMMBW_INST_N=n) so the build compiles them in parallel.
 // The pointers returned here are the kernels' host stubs, registered by their own unit's module.
 #pragma once
@@ -11,9 +12,11 @@
 namespace hmmbw {
 
 using KernelFn = void (*)(EArgs);
+using GroupFn = void (*)(GroupArgs);
 
 struct Kernels {
     KernelFn estep = nullptr, score = nullptr;
+    GroupFn group_estep = nullptr, group_score = nullptr;  // grouped launches (LDS tables only)
 };
 
 // E-step and scorer kernels for N states (1 <= N <= 16), left-to-right or dense, with or without the

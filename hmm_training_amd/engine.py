@@ -249,3 +249,83 @@ class BaumWelchEngine:
 
     def __exit__(self, *exc):
         self.close()
+
+
+class EngineGroup:
+    """Several single-rank engines of one shape (same N, M, resolved topology, device and stream),
+    advanced by ONE grouped E-step launch per EM iteration and scored by one launch (hmmbw_group_*).
+
+    Replaces the per-word training loop of HMM/main.py:147-152 and the per-(recording, model) scoring
+    loop of HMM/hmm_testing.py:139-161.  Every member keeps its own parameters, statistics and stop
+    rule (hmm_training.py:346), so each ends exactly where training it alone would."""
+
+    def __init__(self, engines: Sequence[BaumWelchEngine]):
+        self._lib = lib()
+        self.engines = list(engines)
+        n = len(self.engines)
+        arr = (ctypes.c_void_p * max(n, 1))(*[e._ctx.value for e in self.engines])
+        g = ctypes.c_void_p()
+        check(self._lib.hmmbw_group_create(arr, n, ctypes.byref(g)))
+        self._g = g
+
+    def enqueue_iterations(self, n: int) -> None:
+        check(self._lib.hmmbw_group_iterate(self._g, int(n)))
+
+    def train(self, epsilon: float = 1e-6, max_iterations: int = 100,
+              on_iteration: Optional[Callable[[int, int, float, float], None]] = None,
+              max_chunk: int = 32) -> List[Status]:
+        """EM on every member to its own stop rule; on_iteration(member, k, L_k, diff_k)."""
+        for e in self.engines:
+            e.reset(epsilon, max_iterations)
+        reported = [0] * len(self.engines)
+        chunk = 1
+        while True:
+            sts = [e.status()[0] for e in self.engines]
+            live = [s for s in sts if not s.done]
+            if not live:
+                break
+            n = max(1, min(chunk, int(max_iterations) - min(s.iterations for s in live)))
+            self.enqueue_iterations(n)
+            for i, e in enumerate(self.engines):
+                st, _ = e.status()
+                if on_iteration is not None and st.iterations > reported[i]:
+                    st, recs = e.status(reported[i], st.iterations - reported[i])
+                    for k, (L, d) in enumerate(recs):
+                        on_iteration(i, reported[i] + k, L, d)
+                reported[i] = st.iterations
+            chunk = min(chunk * 2, max_chunk)
+        return [e.status()[0] for e in self.engines]
+
+    def score(self) -> List[np.ndarray]:
+        """Forward-only log P(O_r | lambda_m) of every member's sequences, one launch."""
+        total = sum(e.n_seq for e in self.engines)
+        out = np.zeros(max(total, 1))
+        check(self._lib.hmmbw_group_score(self._g, out.ctypes.data))
+        res, off = [], 0
+        for e in self.engines:
+            res.append(out[off: off + e.n_seq].copy())
+            off += e.n_seq
+        return res
+
+    def timing(self, enable: int = -1) -> Tuple[float, int]:
+        ms = ctypes.c_double()
+        n = ctypes.c_int64()
+        check(self._lib.hmmbw_group_timing(self._g, int(enable), ctypes.byref(ms), ctypes.byref(n)))
+        return ms.value, n.value
+
+    def close(self) -> None:
+        if getattr(self, "_g", None):
+            self._lib.hmmbw_group_destroy(self._g)
+            self._g = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()

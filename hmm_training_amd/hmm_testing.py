@@ -1,8 +1,8 @@
 """Forward-only scoring, the drop-in for HMM/hmm_testing.py (calculate_log_likelihood :49-104,
 test_hmm :107-163), on the MI355X engine.
 
-``score_matrix`` is the batched form: every (sequence, model) log-likelihood with one HIP launch per
-model over all test sequences, instead of the reference's per-pair Python forward pass.
+``score_matrix`` is the batched form: every (sequence, model) log-likelihood in one grouped HIP launch,
+instead of the reference's per-pair Python forward pass.
 """
 from __future__ import annotations
 
@@ -11,20 +11,47 @@ from typing import Dict, List, Sequence, Tuple
 
 import numpy as np
 
-from .engine import BaumWelchEngine
+from .engine import BaumWelchEngine, EngineGroup
 from .hmm_classes import HMMTrained
 from .hmm_training import get_observations
 
 
 def score_matrix(observations: Sequence[np.ndarray], models: Sequence[HMMTrained], device=None) -> np.ndarray:
-    """[len(observations), len(models)] log P(O_r | model_m) (hmm_testing.py:49-104 per entry)."""
+    """[len(observations), len(models)] log P(O_r | model_m) (hmm_testing.py:49-104 per entry).
+
+    Models of one shape (N, M, resolved topology) are scored together by ONE grouped launch over all
+    (sequence, model) pairs (hmmbw_group_score); a model the grouped kernel does not take (N > 16,
+    tables too large for LDS) gets its own launch."""
     out = np.full((len(observations), len(models)), -np.inf)
-    for m, hmm in enumerate(models):
-        N, M = int(hmm.states), int(np.asarray(hmm.B).shape[1])
-        with BaumWelchEngine(N, M, device=device) as eng:
+    if len(observations) == 0 or len(models) == 0:
+        return out
+    engines = []
+    try:
+        for hmm in models:
+            N, M = int(hmm.states), int(np.asarray(hmm.B).shape[1])
+            eng = BaumWelchEngine(N, M, device=device)
+            engines.append(eng)
             eng.set_observations(observations)
             eng.set_params(np.asarray(hmm.Pi), np.asarray(hmm.A), np.asarray(hmm.B))
-            out[:, m] = eng.score()
+        buckets = {}
+        for m, eng in enumerate(engines):
+            key = (eng.N, eng.M, eng.topology) if eng.N <= 16 else ("single", m)
+            buckets.setdefault(key, []).append(m)
+        for members in buckets.values():
+            try:
+                grp = EngineGroup([engines[m] for m in members])
+            except Exception:
+                grp = None
+            if grp is None:
+                for m in members:
+                    out[:, m] = engines[m].score()
+                continue
+            with grp:
+                for m, col in zip(members, grp.score()):
+                    out[:, m] = col
+    finally:
+        for eng in engines:
+            eng.close()
     return out
 
 

@@ -129,11 +129,8 @@ def _dist_context(group=None):
     return 0, 1, None
 
 
-def hmm_training(observations: List[np.ndarray], N: int = 4, M: int = 256, epsilon: float = 1e-6,
-                 max_iterations: int = 100, show_progress=True, word_name: str = None,
-                 load_initial_params: bool = True, *, device: Optional[int] = None, topology: str = "auto",
-                 group=None) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
-    """Baum-Welch EM for one discrete HMM; returns (A, B, pi) like hmm_training.py:265-541."""
+def _initial_params(N: int, M: int, word_name, load_initial_params: bool, show_progress):
+    """Warm start or defaults, with the reference's messages (hmm_training.py:270-325)."""
     pi0 = A0 = B0 = None
     if load_initial_params and word_name:
         loaded = _load_warm_start(word_name, N, M, show_progress)
@@ -152,6 +149,28 @@ def hmm_training(observations: List[np.ndarray], N: int = 4, M: int = 256, epsil
         B0 = dB
         if show_progress:
             print("Using default emission matrix")
+    return pi0, A0, B0
+
+
+def _final_lines(st, max_iterations: int) -> None:
+    """The closing lines of hmm_training.py:516-521 (and its unbound-local error when no iteration ran)."""
+    if st.iterations == 0:
+        # the reference's while-loop never ran: :517 reads an unbound local
+        raise UnboundLocalError("local variable 'current_log_likelihood_sum' referenced before assignment")
+    L, diff = st.last_log_likelihood, st.last_diff
+    print(f"Log-likelihood: {L:.6f}, Diff: {diff:.8f}")
+    if st.iterations >= max_iterations:
+        print(f"Reached maximum iterations ({max_iterations})")
+    else:
+        print(f"Converged after {st.iterations} iterations")
+
+
+def hmm_training(observations: List[np.ndarray], N: int = 4, M: int = 256, epsilon: float = 1e-6,
+                 max_iterations: int = 100, show_progress=True, word_name: str = None,
+                 load_initial_params: bool = True, *, device: Optional[int] = None, topology: str = "auto",
+                 group=None) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+    """Baum-Welch EM for one discrete HMM; returns (A, B, pi) like hmm_training.py:265-541."""
+    pi0, A0, B0 = _initial_params(N, M, word_name, load_initial_params, show_progress)
 
     rank, world, group = _dist_context(group)
     obs = list(observations)
@@ -178,17 +197,96 @@ def hmm_training(observations: List[np.ndarray], N: int = 4, M: int = 256, epsil
         if st.iterations == 0:
             # the reference's while-loop never ran: :517 reads an unbound local
             raise UnboundLocalError("local variable 'current_log_likelihood_sum' referenced before assignment")
-        L, diff = st.last_log_likelihood, st.last_diff
-        if st.iterations >= max_iterations:
-            print(f"Log-likelihood: {L:.6f}, Diff: {diff:.8f}")
-            print(f"Reached maximum iterations ({max_iterations})")
-        else:
-            print(f"Log-likelihood: {L:.6f}, Diff: {diff:.8f}")
-            print(f"Converged after {st.iterations} iterations")
+        _final_lines(st, max_iterations)
         pi, A, B = engine.params(normalise=True)
     finally:
         engine.close()
     return A, B, pi
+
+
+def hmm_training_group(observation_sets: Sequence[List[np.ndarray]], N: int = 4, M: int = 256,
+                       epsilon: float = 1e-6, max_iterations: int = 100, show_progress=True,
+                       word_names: Optional[Sequence[Optional[str]]] = None, load_initial_params: bool = True, *,
+                       device: Optional[int] = None, topology: str = "auto",
+                       stdout_parts: Optional[List[str]] = None) -> List[Tuple[np.ndarray, np.ndarray, np.ndarray]]:
+    """``hmm_training`` for several word models at once (the loop of HMM/main.py:147-152).
+
+    The models of one shape train together: ONE grouped E-step launch per EM iteration
+    (hmmbw_group_iterate) instead of one training run per word.  Each model keeps its own stop rule,
+    so every returned (A, B, pi) equals what ``hmm_training`` returns for that word alone.  The
+    printed lines are each word's own, in word order, as if the words had been trained one after
+    another; with ``stdout_parts`` they are returned per word instead of printed.  Models that
+    cannot be grouped (N > 16, tables too large for LDS, several ranks) train one by one."""
+    import contextlib
+    import io
+
+    from .engine import EngineGroup
+
+    n = len(observation_sets)
+    names = list(word_names) if word_names is not None else [None] * n
+    bufs = [io.StringIO() for _ in range(n)]
+    rank, world, _ = _dist_context(None)
+    if world > 1:  # data-parallel ranks: each word's run is itself sharded (hmm_training)
+        out = []
+        for i, obs in enumerate(observation_sets):
+            with contextlib.redirect_stdout(bufs[i]):
+                out.append(hmm_training(obs, N, M, epsilon, max_iterations, show_progress, names[i],
+                                        load_initial_params, device=device, topology=topology))
+        if stdout_parts is not None:
+            stdout_parts.extend(b.getvalue() for b in bufs)
+        else:
+            for b in bufs:
+                print(b.getvalue(), end="")
+        return out
+    engines: List[Optional[BaumWelchEngine]] = [None] * n
+    results: List[Optional[Tuple[np.ndarray, np.ndarray, np.ndarray]]] = [None] * n
+    try:
+        for i, obs in enumerate(observation_sets):
+            with contextlib.redirect_stdout(bufs[i]):
+                pi0, A0, B0 = _initial_params(N, M, names[i], load_initial_params, show_progress)
+            eng = BaumWelchEngine(N, M, device=device, topology=topology)
+            engines[i] = eng
+            eng.set_observations(list(obs))
+            eng.set_params(pi0, A0, B0)
+        groupable = N <= 16
+        buckets = {}
+        for i, eng in enumerate(engines):
+            buckets.setdefault(eng.topology if groupable else i, []).append(i)
+        statuses = [None] * n
+        for members in buckets.values():
+            def report(m: int, k: int, L: float, diff: float, members=members) -> None:
+                if show_progress:
+                    bufs[members[m]].write(f"Iteration {k + 1}\nLog-likelihood: {L:.6f}, Diff: {diff:.8f}\n")
+            try:
+                grp = EngineGroup([engines[i] for i in members])
+            except Exception:  # shape the grouped kernel does not take: train one by one
+                grp = None
+            if grp is not None:
+                with grp:
+                    sts = grp.train(epsilon, max_iterations, report)
+            else:
+                sts = []
+                for m, i in enumerate(members):
+                    sts.append(engines[i].train(epsilon, max_iterations,
+                                                lambda k, L, d, m=m: report(m, k, L, d)))
+            for m, i in enumerate(members):
+                statuses[i] = sts[m]
+        for i, eng in enumerate(engines):
+            st = statuses[i]
+            with contextlib.redirect_stdout(bufs[i]):
+                _final_lines(st, max_iterations)
+            pi, A, B = eng.params(normalise=True)
+            results[i] = (A, B, pi)
+    finally:
+        for eng in engines:
+            if eng is not None:
+                eng.close()
+    if stdout_parts is not None:
+        stdout_parts.extend(b.getvalue() for b in bufs)
+    else:
+        for b in bufs:
+            print(b.getvalue(), end="")
+    return results
 
 
 def training_with_save(word_recordings, centroids, word_name: str, max_iterations=100, show_progress=True,

@@ -8,16 +8,22 @@ Same on-disk layout as the reference:
 * ``<data>/<TrainHMM|Test>/<word>/<recording>/*_frames.json`` — the recordings;
 * ``<data>/ResultsHMM/<word>.json`` — the trained models (DataStorageHMM's default directory).
 
-The same messages are printed. Two things differ:
-* training goes through the drop-in ``training_with_save`` (the Baum-Welch HIP engine);
-* testing goes through ``test_hmm`` (one scoring launch per model).
+The same messages are printed, in the same order. Two things differ:
+* training runs every word model together, one grouped E-step launch per EM iteration
+  (``hmm_training_group``; each model still stops on its own rule, so the saved models equal the
+  reference's word-by-word training); ``grouped=False`` trains word by word through the drop-in
+  ``training_with_save``;
+* testing goes through ``test_hmm`` (one scoring launch for all (recording, model) pairs).
 The confusion-matrix plot (``create_confusion_matrix``, matplotlib) is out of scope; ``test``
 returns the labels instead.
 """
 from __future__ import annotations
 
 import argparse
+import contextlib
+import io
 import logging
+import sys
 import os
 import random
 from collections import defaultdict
@@ -26,7 +32,7 @@ from typing import Dict, List, Optional
 
 from .hmm_classes import DataStorageHMM, HMMTrained
 from .hmm_testing import test_hmm
-from .hmm_training import training_with_save
+from .hmm_training import get_observations, hmm_training_group, training_with_save
 from .io import Centroid, Frame, load_centroids, load_frames
 
 logger = logging.getLogger(__name__)
@@ -87,8 +93,47 @@ def load_mfcc_centroids(base_dir="../Data", print_messages=True) -> List[Centroi
     return centroids
 
 
+def _train_grouped(recordings_by_word, centroids, show_progress, max_iterations, load_initial_params,
+                   model_dir, n_states=4) -> Optional[List[HMMTrained]]:
+    """All words in one group (hmm_training_group), printing each word's lines in word order exactly
+    as the word-by-word loop does.  None when the grouped run cannot start (the caller then runs the
+    word-by-word loop, which reproduces the reference's partial output and error for bad input)."""
+    heads, obs_sets, words = [], [], []
+    try:
+        for word_name, word_recordings in recordings_by_word.items():
+            buf = io.StringIO()
+            with contextlib.redirect_stdout(buf):
+                print(f"\nTraining HMM for word: '{word_name}' with {len(word_recordings)} recordings")
+                print("Converting recordings to observations...")  # training_with_save, hmm_training.py:215-247
+                observations = get_observations(word_recordings, centroids)
+                print(f"Generated {len(observations)} observation sequences")
+                print(f"Sequence lengths: {[len(obs) for obs in observations]}")
+                print("Starting Baum-Welch training...")
+            heads.append(buf.getvalue())
+            obs_sets.append(observations)
+            words.append(word_name)
+        parts: List[str] = []
+        results = hmm_training_group(obs_sets, N=n_states, M=len(centroids), max_iterations=max_iterations,
+                                     show_progress=show_progress, word_names=words,
+                                     load_initial_params=load_initial_params, stdout_parts=parts)
+    except Exception:
+        return None
+    trained = []
+    for i, word_name in enumerate(words):
+        sys.stdout.write(heads[i] + parts[i])
+        A, B, pi = results[i]
+        model = HMMTrained(states=n_states, symbols=len(centroids), A=A, B=B, Pi=pi, word=word_name)
+        if model_dir is None:
+            DataStorageHMM.save_hmm(model, print_messages=False)
+        else:
+            DataStorageHMM.save_hmm(model, base_dir=model_dir, print_messages=False)
+        trained.append(model)
+        print(f"Model saved for word: '{model.word}'")
+    return trained
+
+
 def train_hmm(show_progress=True, max_iterations=100, load_initial_params=False, base_dir="../Data",
-              model_dir: Optional[str] = None) -> Optional[List[HMMTrained]]:
+              model_dir: Optional[str] = None, grouped: bool = True) -> Optional[List[HMMTrained]]:
     """Train one HMM per word (main.py:133-164); None on any error, as the reference."""
     print("Starting HMM training for all words...")
     try:
@@ -96,8 +141,16 @@ def train_hmm(show_progress=True, max_iterations=100, load_initial_params=False,
         print(f"Loaded {len(centroids)} centroids")
         recordings_by_word = load_all_recordings_by_word(base_dir, purpose="TrainHMM", print_messages=False)
         print(f"Loaded recordings for {len(recordings_by_word)} words")
-        trained = []
-        for word_name, word_recordings in recordings_by_word.items():
+        trained = None
+        if grouped:
+            trained = _train_grouped(recordings_by_word, centroids, show_progress, max_iterations,
+                                     load_initial_params, model_dir)
+        if trained is None:  # word by word (the reference's loop, main.py:147-152)
+            trained = []
+            words = recordings_by_word.items()
+        else:
+            words = ()
+        for word_name, word_recordings in words:
             print(f"\nTraining HMM for word: '{word_name}' with {len(word_recordings)} recordings")
             model = training_with_save(word_recordings, centroids, word_name, max_iterations=max_iterations,
                                        show_progress=show_progress, load_initial_params=load_initial_params,

@@ -150,6 +150,27 @@ int hmmbw_set_option(hmmbw_ctx *ctx, int key, int64_t value);
  * overhead out of the timed loop); enable < 0 only queries. */
 int hmmbw_timing(hmmbw_ctx *ctx, int enable, double *total_ms, int64_t *count);
 
+/* ---- Groups: several models of one shape, one launch per EM iteration / per scoring pass ----
+ * The reference trains its word models one after another (train_hmm, HMM/main.py:147-152, calling
+ * training_with_save -> hmm_training once per word, hmm_training.py:215-247) and scores every
+ * (recording, model) pair with its own forward pass (test_hmm, HMM/hmm_testing.py:139-161).  A group
+ * advances all member contexts with ONE grouped E-step launch per iteration (each member's M-step runs
+ * in its slice's prologue; each member keeps its own parameters, statistics, convergence state and
+ * stop rule, exactly as if trained alone) and scores all of them with one launch.
+ * Members: single-rank contexts on the same device and stream, with equal N, M and resolved topology,
+ * N <= 16 and emission tables that fit LDS, each with observations and parameters set (checked at
+ * creation, HMMBW_E_UNSUPPORTED otherwise, and again at every call); the group does not own them
+ * (destroy the group first). */
+typedef struct hmmbw_group hmmbw_group;
+int hmmbw_group_create(hmmbw_ctx *const *ctxs, int n, hmmbw_group **out);
+int hmmbw_group_destroy(hmmbw_group *group);
+/* hmmbw_iterate(ctx, n_iter) for every member (arm each with hmmbw_reset_training first). */
+int hmmbw_group_iterate(hmmbw_group *group, int64_t n_iter);
+/* SYNC. hmmbw_score of every member, concatenated in member order (sum of the members' R doubles). */
+int hmmbw_group_score(hmmbw_group *group, double *out);
+/* Timing of the grouped E-step launches (same protocol as hmmbw_timing). */
+int hmmbw_group_timing(hmmbw_group *group, int enable, double *total_ms, int64_t *count);
+
 #ifdef __cplusplus
 }
 #endif
