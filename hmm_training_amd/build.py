@@ -28,7 +28,8 @@ SMALL_N = range(1, 17)
 
 def units():
     """(source, extra defines, object stem) of every translation unit."""
-    u = [(SRC, [], "hmmbw"), (os.path.join(CSRC, "estep_wide_inst.hip"), [], "estep_wide")]
+    u = [(SRC, [], "hmmbw"), (os.path.join(CSRC, "estep_wide_inst.hip"), [], "estep_wide"),
+         (os.path.join(CSRC, "vq.hip"), [], "vq")]
     u += [(os.path.join(CSRC, "estep_small_inst.hip"), [f"-DHMMBW_INST_N={n}"], f"estep_small_n{n}")
           for n in SMALL_N]
     return u

@@ -49,7 +49,7 @@ __global__ void __launch_bounds__(NT * 64) k_estep_mfma(EArgs a) {
     constexpr int NP = 16 * NT, KB = 4 * NT, IMG = NP * kXs;
     extern __shared__ double smem[];
     double *X0 = smem;                                   // [2][NP][kXs]: z (forward) / V (backward)
-    double *X1 = smem + 2 * IMG;                         // [2][NP][kXs]: masked z (backward xi operand)
+    // smem + 2 * IMG: [2][NP][kXs] masked z (backward xi operand), addressed as putb / topb + 2 * IMG
     double *sRed = smem + (FWD_ONLY ? 2 : 4) * IMG;      // [NT][16] partial sums + block LL scratch
     if (a.state != nullptr && a.state->done) return;    // converged: device-side no-op (:346)
     const int tid = threadIdx.x, lane = tid & 63, m = tid >> 6;

@@ -1035,6 +1035,22 @@ int group_launch(hmmbw_group *g, const std::vector<Plan> &plans, int n_launch, b
 
 extern "C" {
 
+int hmmbw_vq_encode(void *stream, const double *frames, int64_t n_frames, int frame_stride, int first_dim, int dims,
+                    const double *centroids, int n_centroids, int32_t *symbols, double *distances) {
+    if (n_frames < 0) return fail(HMMBW_E_INVALID, "negative frame count");
+    if (n_frames == 0) return HMMBW_OK;
+    if (!frames || !centroids || !symbols) return fail(HMMBW_E_INVALID, "null argument");
+    if (dims < 1 || dims > 64 || first_dim < 0 || frame_stride < first_dim + dims)
+        return fail(HMMBW_E_INVALID, "need 1 <= dims <= 64 and first_dim + dims <= frame_stride");
+    if (n_centroids < 1) return fail(HMMBW_E_INVALID, "empty codebook");
+    if ((long long)n_centroids * dims > 20480) return fail(HMMBW_E_UNSUPPORTED, "codebook larger than 160 KiB of LDS");
+    if (n_frames > (1LL << 40)) return fail(HMMBW_E_UNSUPPORTED, "too many frames");
+    hipError_t e = launch_vq(reinterpret_cast<hipStream_t>(stream), frames, n_frames, frame_stride, first_dim, dims,
+                             centroids, n_centroids, symbols, distances);
+    if (e != hipSuccess) return fail(HMMBW_E_HIP, std::string("vq launch: ") + hipGetErrorString(e));
+    return HMMBW_OK;
+}
+
 int hmmbw_group_create(hmmbw_ctx *const *ctxs, int n, hmmbw_group **out) {
     if (!out || (!ctxs && n > 0)) return fail(HMMBW_E_INVALID, "null argument");
     if (n <= 0) return fail(HMMBW_E_INVALID, "a group needs at least one context");

@@ -31,4 +31,8 @@ Kernels wide_kernels(int NP);
 using BnumFn = void (*)(const double *, const unsigned *, const long long *, int, int, double *, const IterState *);
 BnumFn bnum_gather_kernel();
 
+// The VQ encoder (vq.hip).
+hipError_t launch_vq(hipStream_t st, const double *frames, long long n_frames, int stride, int col0, int dims,
+                     const double *centroids, int n_centroids, int *symbols, double *dist);
+
 }  // namespace hmmbw

@@ -1,0 +1,83 @@
+// vq.hip — vector-quantisation encoder (the step before the Baum-Welch path) for gfx950.
+//
+// Replaces get_observations, HMM/hmm_training.py:82-120: for every frame, the index of the nearest
+// centroid by Euclidean distance over the MFCC coefficients [1, 13) (the power coefficient 0 is
+// skipped, :98 and :106), scanning centroids in order and keeping the FIRST minimum (strict '<',
+// :111).  Bit-exact with the reference: its distance is np.linalg.norm(frame - centroid) (:109) =
+// sqrt(x.dot(x)), and for these 12-element vectors OpenBLAS's ddot is a sequential fused
+// multiply-add from element 0 (its vector kernel starts at 32 elements); oracle/bw_oracle.c restates
+// that and tests/test_oracle_golden.py pins it to numpy bit for bit.  So each distance here is
+//     d = fma(x_11, x_11, ... fma(x_1, x_1, x_0 * x_0)),  x_i = f_i - c_i,   s = sqrt(d)
+// with the correctly rounded fp64 sqrt, and the comparison is on s, as in the reference (two
+// different d can round to the same s, and then the earlier centroid wins).  sqrt is monotone, so
+// s < s_best needs d < d_best: the sqrt is only evaluated for those candidates.
+//
+// Mapping: one lane per frame (fp64 VALU; the scan is a dependent fma chain per centroid, not a
+// GEMM: a -2 f.c + |c|^2 reformulation would round differently).  Every lane of a wave scans the same
+// centroid at the same time, so the centroid is a wave-uniform operand: the workgroup stages the
+// codebook in LDS once and each centroid row is a broadcast read.  The frame's D values stay in
+// registers.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+
+namespace hmmbw {
+
+template <int DMAX>
+__global__ void __launch_bounds__(256) k_vq_encode(const double *__restrict__ frames, long long F, int stride,
+                                                   int col0, int D, const double *__restrict__ cents, int K,
+                                                   int *__restrict__ out, double *__restrict__ dist) {
+    extern __shared__ double sC[];  // [K][D] codebook (columns col0 .. col0 + D)
+    for (int i = threadIdx.x; i < K * D; i += blockDim.x) {
+        const int k = i / D, d = i - k * D;
+        sC[i] = cents[(long long)k * stride + col0 + d];
+    }
+    __syncthreads();
+    const long long f = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (f >= F) return;
+    double x[DMAX];
+#pragma unroll
+    for (int d = 0; d < DMAX; ++d) x[d] = (d < D) ? frames[f * stride + col0 + d] : 0.0;
+    double best_s = INFINITY, best_d = INFINITY;
+    int arg = 0;
+    for (int k = 0; k < K; ++k) {
+        const double *c = sC + k * D;
+        double acc = 0.0;
+#pragma unroll
+        for (int d = 0; d < DMAX; ++d) {
+            if (DMAX > 16 && d >= D) break;
+            const double e = x[d] - c[d];
+            acc = (d == 0) ? e * e : __builtin_fma(e, e, acc);
+        }
+        if (acc < best_d) {  // the only candidates whose sqrt can be below best_s (sqrt is monotone)
+            const double s = __builtin_sqrt(acc);
+            if (s < best_s) {
+                best_s = s;
+                best_d = acc;
+                arg = k;
+            }
+        }
+    }
+    out[f] = arg;
+    if (dist) dist[f] = best_s;  // the reference's min_distance (:112)
+}
+
+
+// Enqueue the encoder (arguments validated by hmmbw_vq_encode in hmmbw.hip).
+hipError_t launch_vq(hipStream_t st, const double *frames, long long n_frames, int stride, int col0, int dims,
+                     const double *centroids, int n_centroids, int *symbols, double *dist) {
+    const size_t lds = sizeof(double) * (size_t)n_centroids * dims;
+    const unsigned grid = (unsigned)((n_frames + 255) / 256);
+    auto f = dims == 12 ? k_vq_encode<12> : k_vq_encode<64>;
+    if (lds > 64 * 1024) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(f),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(f, dim3(grid), dim3(256), lds, st, frames, n_frames, stride, col0, dims, centroids,
+                       n_centroids, symbols, dist);
+    return hipGetLastError();
+}
+
+}  // namespace hmmbw

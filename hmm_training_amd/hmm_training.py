@@ -5,7 +5,7 @@ Same names, signatures, printed lines, return order and error behaviour as the r
 * ``hmm_training(observations, N=4, M=256, epsilon=1e-6, max_iterations=100, show_progress=True,
   word_name=None, load_initial_params=True) -> (A, B, pi)``            (hmm_training.py:265-541)
 * ``training_with_save(word_recordings, centroids, word_name, ...) -> HMMTrained`` (:215-247)
-* ``get_observations(recordings, centroids)``                            (:82-120)
+* ``get_observations(recordings, centroids)``                            (:82-120, HIP encoder)
 * ``safe_log`` / ``safe_exp`` / ``log_sum_exp``                          (:46-79)
 
 The EM iterations run in hand-written HIP kernels (hmm_training_amd/csrc/hmmbw.hip) through the C
@@ -59,22 +59,64 @@ def log_sum_exp(log_probs):
     return log_probs if log_probs != float("-inf") else float("-inf")
 
 
-def get_observations(recordings, centroids) -> List[np.ndarray]:
+def get_observations(recordings, centroids, device: Optional[int] = None) -> List[np.ndarray]:
     """Vector quantisation (hmm_training.py:82-120): per frame, the index of the nearest centroid by
-    Euclidean distance over mfcc[1:] (power coefficient excluded), first minimum on ties."""
+    Euclidean distance over mfcc[1:] (power coefficient excluded), first minimum on ties.  All frames
+    of all recordings go through ONE launch of the HIP encoder (hmmbw_vq_encode), whose distances are
+    computed exactly as np.linalg.norm does, so the indices are the reference's bit for bit."""
     if len(centroids) == 0:
         return [np.zeros(len(r), dtype=np.int64) for r in recordings]
-    C = np.stack([np.asarray(c.mfcc, dtype=np.float64)[1:] for c in centroids])
-    out = []
-    for rec in recordings:
-        if len(rec) == 0:
-            out.append(np.array([]))
-            continue
-        F = np.stack([np.asarray(f.mfcc, dtype=np.float64)[1:] for f in rec])
-        diff = F[:, None, :] - C[None, :, :]
-        dist = np.sqrt(np.einsum("fkd,fkd->fk", diff, diff))
-        out.append(np.argmin(dist, axis=1).astype(np.int64))
+    C = np.stack([np.asarray(c.mfcc, dtype=np.float64).reshape(-1) for c in centroids])
+    lengths = [len(r) for r in recordings]
+    frames = [np.asarray(f.mfcc, dtype=np.float64).reshape(-1) for rec in recordings for f in rec]
+    if not frames:
+        return [np.array([]) for _ in recordings]
+    Fm = np.stack(frames)
+    if Fm.shape[1] != C.shape[1]:
+        raise ValueError(f"operands could not be broadcast together with shapes ({Fm.shape[1] - 1},) "
+                         f"({C.shape[1] - 1},)")
+    symbols = vq_encode(Fm, C, device=device)
+    out, pos = [], 0
+    for T in lengths:
+        out.append(symbols[pos:pos + T].astype(np.int64) if T else np.array([]))
+        pos += T
     return out
+
+
+def vq_encode(frames: np.ndarray, centroids: np.ndarray, device: Optional[int] = None, first_dim: int = 1,
+              return_distances: bool = False):
+    """[F] nearest-centroid indices (int64) of frames [F][D] against centroids [K][D] over the columns
+    [first_dim, D) on the GPU (hmmbw_vq_encode, include/hmmbw.h)."""
+    import ctypes
+
+    import torch
+
+    from ._lib import check, lib
+    frames = np.ascontiguousarray(frames, dtype=np.float64)
+    centroids = np.ascontiguousarray(centroids, dtype=np.float64)
+    F, D = frames.shape
+    K = centroids.shape[0]
+    dims = D - first_dim
+    if F == 0:
+        return (np.zeros(0, np.int64), np.zeros(0)) if return_distances else np.zeros(0, np.int64)
+    if dims <= 0:  # every distance is norm([]) = 0: the first centroid wins
+        z = np.zeros(F, dtype=np.int64)
+        return (z, np.zeros(F)) if return_distances else z
+    dev = torch.device("cuda", torch.cuda.current_device() if device is None else int(device))
+    L = lib()
+    with torch.cuda.device(dev):
+        tf = torch.from_numpy(frames).to(dev)
+        tc = torch.from_numpy(centroids).to(dev)
+        ts = torch.empty(F, dtype=torch.int32, device=dev)
+        td = torch.empty(F, dtype=torch.float64, device=dev) if return_distances else None
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        check(L.hmmbw_vq_encode(ctypes.c_void_p(stream), ctypes.c_void_p(tf.data_ptr()), F, D, first_dim, dims,
+                                ctypes.c_void_p(tc.data_ptr()), K, ctypes.c_void_p(ts.data_ptr()),
+                                ctypes.c_void_p(td.data_ptr()) if td is not None else None))
+        sym = ts.cpu().numpy().astype(np.int64)
+        if return_distances:
+            return sym, td.cpu().numpy()
+    return sym
 
 
 def default_initial_params(N: int, M: int) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:

@@ -150,6 +150,18 @@ int hmmbw_set_option(hmmbw_ctx *ctx, int key, int64_t value);
  * overhead out of the timed loop); enable < 0 only queries. */
 int hmmbw_timing(hmmbw_ctx *ctx, int enable, double *total_ms, int64_t *count);
 
+/* Vector-quantisation encoder: get_observations, hmm_training.py:82-120.  For every frame f, the index
+ * of the nearest centroid (first minimum, strict '<' as at :111) by the Euclidean distance over the
+ * columns [first_dim, first_dim + dims) of frames[f * frame_stride ...] and centroids[k * frame_stride
+ * ...] (the reference: stride 13, first_dim 1 — mfcc[1:] without the power coefficient — dims 12),
+ * computed exactly as np.linalg.norm does (sequential fused multiply-add, correctly rounded sqrt), so
+ * the indices are bit-identical to the reference's.  DEVICE pointers (frames [n_frames][stride],
+ * centroids [n_centroids][stride] fp64, symbols int32 [n_frames], distances fp64 [n_frames] or NULL:
+ * the winning distance, the reference's min_distance); enqueued on `stream` (hipStream_t, NULL =
+ * legacy default), asynchronous; the device is the current one.  Codebook <= 160 KiB. */
+int hmmbw_vq_encode(void *stream, const double *frames, int64_t n_frames, int frame_stride, int first_dim, int dims,
+                    const double *centroids, int n_centroids, int32_t *symbols, double *distances);
+
 /* ---- Groups: several models of one shape, one launch per EM iteration / per scoring pass ----
  * The reference trains its word models one after another (train_hmm, HMM/main.py:147-152, calling
  * training_with_save -> hmm_training once per word, hmm_training.py:215-247) and scores every

@@ -304,16 +304,25 @@ int oracle_forward_loglik(const int64_t *offsets, const int64_t *symbols, int64_
 
 /* hmm_training.py:82-120 get_observations: nearest centroid by Euclidean distance over
  * mfcc[1:], first minimum wins (strict '<' at :112). frames [F][D], centroids [K][D]. */
-void oracle_vq(const double *frames, int64_t F, const double *centroids, int64_t K, int D, int64_t *out) {
+void oracle_vq(const double *frames, int64_t F, const double *centroids, int64_t K, int D, int64_t *out,
+               double *dist_out) {
+    /* hmm_training.py:94-114.  distance = np.linalg.norm(frame[1:] - centroid[1:]) (:109) =
+     * sqrt(x.dot(x)); OpenBLAS ddot on these 12-element vectors is a sequential fused multiply-add
+     * from element 0 (measured bit-exact against numpy here: tests/test_oracle_golden.py).  First
+     * minimum wins (strict '<', :111); NaN distances never win, so the index stays 0. */
     for (int64_t f = 0; f < F; ++f) {
         double best = INFINITY;
         int64_t arg = 0;
         for (int64_t k = 0; k < K; ++k) {
             double s = 0.0;
-            for (int d = 1; d < D; ++d) { double e = frames[f * D + d] - centroids[k * D + d]; s += e * e; }
-            double dist = sqrt(s);
+            for (int d = 1; d < D; ++d) {
+                const double e = frames[f * D + d] - centroids[k * D + d];
+                s = fma(e, e, s);
+            }
+            const double dist = sqrt(s);
             if (dist < best) { best = dist; arg = k; }
         }
         out[f] = arg;
+        if (dist_out) dist_out[f] = best;
     }
 }

@@ -42,7 +42,7 @@ def load():
         lib.oracle_forward_loglik.argtypes = [_ip, _ip, ctypes.c_int64, ctypes.c_int, ctypes.c_int, _dp, _dp, _dp,
                                               _dp]
         lib.oracle_vq.restype = None
-        lib.oracle_vq.argtypes = [_dp, ctypes.c_int64, _dp, ctypes.c_int64, ctypes.c_int, _ip]
+        lib.oracle_vq.argtypes = [_dp, ctypes.c_int64, _dp, ctypes.c_int64, ctypes.c_int, _ip, _dp]
         lib.oracle_lse.restype = ctypes.c_double
         lib.oracle_lse.argtypes = [_dp, ctypes.c_int64]
         _lib = lib
@@ -117,13 +117,15 @@ def forward_loglik(offsets, symbols, N, M, pi, A, B) -> np.ndarray:
     return out[:R]
 
 
-def vq(frames: np.ndarray, centroids: np.ndarray) -> np.ndarray:
+def vq(frames: np.ndarray, centroids: np.ndarray, return_dist: bool = False):
+    """Nearest-centroid index over columns [1, D) (hmm_training.py:82-120); frames [F][D], centroids [K][D]."""
     lib = load()
     frames = np.ascontiguousarray(frames, np.float64)
     centroids = np.ascontiguousarray(centroids, np.float64)
     out = np.zeros(len(frames), dtype=np.int64)
-    lib.oracle_vq(frames, len(frames), centroids, len(centroids), frames.shape[1], out)
-    return out
+    dist = np.zeros(len(frames), dtype=np.float64)
+    lib.oracle_vq(frames, len(frames), centroids, len(centroids), frames.shape[1], out, dist)
+    return (out, dist) if return_dist else out
 
 
 def lse(x) -> float:

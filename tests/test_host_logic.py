@@ -101,16 +101,6 @@ def test_csr_and_shards():
         assert max(loads) - min(loads) <= 2 * lengths.max()
 
 
-def test_get_observations_matches_reference_vq():
-    from types import SimpleNamespace as NS
-    from hmm_training_amd.hmm_training import get_observations
-    d = np.load(os.path.join(GOLDEN, "vq_k64.npz"), allow_pickle=False)
-    off = d["offsets"]
-    recs = [[NS(mfcc=f) for f in d["frames"][off[i]:off[i + 1]]] for i in range(len(off) - 1)]
-    out = get_observations(recs, [NS(mfcc=c) for c in d["centroids"]])
-    assert np.array_equal(np.concatenate(out), d["symbols"])
-
-
 def test_stats_layout_roundtrip():
     from hmm_training_amd.engine import StatsLayout
     L = StatsLayout(3, 5, world=2)

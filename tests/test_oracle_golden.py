@@ -55,6 +55,39 @@ def test_oracle_vq(oracle):
     assert np.array_equal(oracle.vq(d["frames"], d["centroids"]), d["symbols"])
 
 
+def reference_vq_loop(frames, cents):
+    """The reference's own loop (hmm_training.py:94-114) with numpy's np.linalg.norm, per pair."""
+    idx, dist = [], []
+    for f in frames:
+        best, arg = float("inf"), 0
+        for k, c in enumerate(cents):
+            dd = np.linalg.norm(f[1:] - c[1:])
+            if dd < best:
+                best, arg = dd, k
+        idx.append(arg)
+        dist.append(best)
+    return np.array(idx), np.array(dist)
+
+
+def test_oracle_vq_distances_bitwise_equal_numpy_norm(oracle):
+    """Pins the oracle's distance arithmetic (sequential fma + sqrt) to numpy's np.linalg.norm, the
+    reference's distance (:109), bit for bit; includes exact ties (duplicate centroids, midpoints),
+    which the first minimum must win, and a NaN frame (index 0)."""
+    rng = np.random.default_rng(123)
+    cents = rng.normal(size=(64, 13)) * rng.uniform(0.5, 20.0, size=(64, 1))
+    cents[10] = cents[3]                                 # duplicate: 3 must win over 10
+    frames = rng.normal(size=(300, 13)) * 8.0
+    frames[:20] = cents[rng.integers(0, 64, size=20)] + 1e-9 * rng.normal(size=(20, 13))
+    frames[20] = 0.5 * (cents[5] + cents[6])             # (near-)equidistant
+    frames[21, 1:] = np.nan
+    frames[22] = cents[3]                                # distance 0 to 3 and 10
+    ref_idx, ref_dist = reference_vq_loop(frames, cents)
+    idx, dist = oracle.vq(frames, cents, return_dist=True)
+    assert np.array_equal(idx, ref_idx)
+    assert np.array_equal(dist.view(np.int64)[np.isfinite(ref_dist)], ref_dist.view(np.int64)[np.isfinite(ref_dist)])
+    assert idx[21] == 0 and idx[22] == 3
+
+
 def test_oracle_estep_stats_consistency(oracle):
     """Sum rules of the E-step statistics: sum_j xi(i,j) = gamma_den_excl(i); sum_k B_num = gamma_den_all."""
     d = load("dense_n6")
