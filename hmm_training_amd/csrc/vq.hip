@@ -14,8 +14,8 @@
 //
 // Mapping: one lane per frame (fp64 VALU; the scan is a dependent fma chain per centroid, not a
 // GEMM: a -2 f.c + |c|^2 reformulation would round differently).  Every lane of a wave scans the same
-// centroid at the same time, so the centroid is a wave-uniform operand: the workgroup stages the
-// codebook in LDS once and each centroid row is a broadcast read.  The frame's D values stay in
+// centroid at the same time, so the centroid is a wave-uniform operand (scalar loads for the
+// reference's 12 dims, an LDS-staged codebook for other widths).  The frame's D values stay in
 // registers.
 #include <hip/hip_runtime.h>
 
@@ -24,6 +24,57 @@
 
 namespace hmmbw {
 
+// DMAX = D (exact, the reference's 12 dims): the codebook is read with wave-uniform SCALAR loads
+// (s_load into SGPRs, one copy per wave, which v_add_f64 takes as its operand), so the scan costs no
+// LDS bandwidth: a broadcast ds_read still returns 8 bytes per lane, and with 24 fp64 VALU ops per
+// (frame, centroid) the LDS return path, not the fp64 pipe, bounded the LDS-staged form (measured).
+template <int D>
+__global__ void __launch_bounds__(256) k_vq_encode_s(const double *__restrict__ frames, long long F, int stride,
+                                                     int col0, const double *__restrict__ cents, int K,
+                                                     int *__restrict__ out, double *__restrict__ dist) {
+    const long long f = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (f >= F) return;
+    double x[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d) x[d] = frames[f * stride + col0 + d];
+    double best_s = INFINITY, best_d = INFINITY;
+    int arg = 0;
+    const double *c = cents + col0;
+    // centroid k + 1's row is loaded (into SGPRs) while centroid k is scanned
+    double cn[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d) cn[d] = c[d];
+    for (int k = 0; k < K; ++k) {
+        double cc[D];
+#pragma unroll
+        for (int d = 0; d < D; ++d) cc[d] = cn[d];
+        c += stride;
+        if (k + 1 < K) {
+#pragma unroll
+            for (int d = 0; d < D; ++d) cn[d] = c[d];
+        }
+        double acc = 0.0;
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            const double e = x[d] - cc[d];
+            acc = (d == 0) ? e * e : __builtin_fma(e, e, acc);
+        }
+        // only candidates with acc < best_d can have sqrt(acc) < best_s (sqrt is monotone); after the
+        // first few centroids that is rare, so the sqrt sits behind a real branch
+        if (__builtin_expect(__any(acc < best_d), 0) && acc < best_d) {
+            const double s = __builtin_sqrt(acc);
+            if (s < best_s) {
+                best_s = s;
+                best_d = acc;
+                arg = k;
+            }
+        }
+    }
+    out[f] = arg;
+    if (dist) dist[f] = best_s;  // the reference's min_distance (:112)
+}
+
+// Any D <= DMAX: codebook staged in LDS.
 template <int DMAX>
 __global__ void __launch_bounds__(256) k_vq_encode(const double *__restrict__ frames, long long F, int stride,
                                                    int col0, int D, const double *__restrict__ cents, int K,
@@ -46,11 +97,11 @@ __global__ void __launch_bounds__(256) k_vq_encode(const double *__restrict__ fr
         double acc = 0.0;
 #pragma unroll
         for (int d = 0; d < DMAX; ++d) {
-            if (DMAX > 16 && d >= D) break;
+            if (d >= D) break;
             const double e = x[d] - c[d];
             acc = (d == 0) ? e * e : __builtin_fma(e, e, acc);
         }
-        if (acc < best_d) {  // the only candidates whose sqrt can be below best_s (sqrt is monotone)
+        if (acc < best_d) {
             const double s = __builtin_sqrt(acc);
             if (s < best_s) {
                 best_s = s;
@@ -60,16 +111,20 @@ __global__ void __launch_bounds__(256) k_vq_encode(const double *__restrict__ fr
         }
     }
     out[f] = arg;
-    if (dist) dist[f] = best_s;  // the reference's min_distance (:112)
+    if (dist) dist[f] = best_s;
 }
-
 
 // Enqueue the encoder (arguments validated by hmmbw_vq_encode in hmmbw.hip).
 hipError_t launch_vq(hipStream_t st, const double *frames, long long n_frames, int stride, int col0, int dims,
                      const double *centroids, int n_centroids, int *symbols, double *dist) {
-    const size_t lds = sizeof(double) * (size_t)n_centroids * dims;
     const unsigned grid = (unsigned)((n_frames + 255) / 256);
-    auto f = dims == 12 ? k_vq_encode<12> : k_vq_encode<64>;
+    if (dims == 12) {
+        hipLaunchKernelGGL(k_vq_encode_s<12>, dim3(grid), dim3(256), 0, st, frames, n_frames, stride, col0, centroids,
+                           n_centroids, symbols, dist);
+        return hipGetLastError();
+    }
+    const size_t lds = sizeof(double) * (size_t)n_centroids * dims;
+    auto f = k_vq_encode<64>;
     if (lds > 64 * 1024) {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(f),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
