@@ -213,7 +213,9 @@ def main():
             "config": {"workload": f"{wl} per GPU: R={R} sequences x T={T}, N={N} states, K={K} symbols, "
                                    f"{args.topology} A, one EM iteration per step",
                        "sequences_per_gpu": R, "T": T, "N": N, "K": K, "topology": args.topology,
-                       "parallelism": f"dp{world}" if world > 1 else "single"},
+                       "parallelism": f"dp{world}" if world > 1 else "single",
+                       "allreduce": ("rccl (engine communicator, engine stream)" if eng.native_comm else
+                                     "torch.distributed") if world > 1 else None},
             "roofline": roof,
             "loglik_last": st.last_log_likelihood,
         }

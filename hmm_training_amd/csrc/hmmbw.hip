@@ -29,6 +29,9 @@
 //   k_mstep / k_mstep_staged  one workgroup: L, M-step, convergence record, zero the statistics
 //                   (staged: all statistics gathered into LDS with one batch of loads).
 //   k_finalise  the reference's return-path normalisation (:524-541).
+#include <dlfcn.h>
+#include <rccl/rccl.h>
+
 #include "hmmbw_device.hpp"
 #include "hmmbw_kernels.hpp"
 
@@ -198,6 +201,10 @@ struct hmmbw_ctx {
     unsigned *d_brows = nullptr;
     uint4 *d_sp = nullptr;
     int *d_ebuf = nullptr;
+    // native RCCL communicator (hmmbw_comm_init): the multi-rank hmmbw_iterate all-reduces d_ext
+    ncclComm_t comm = nullptr;
+    double *d_ext = nullptr;
+    long long R_global = 0;
     bool has_obs = false;
     int force_safe = 0;
     int ablate = 0;
@@ -448,6 +455,45 @@ int check_ready(hmmbw_ctx *c, bool need_armed) {
     return set_device(c);
 }
 
+// RCCL entry points, resolved at run time from the RCCL library already in the process (the one
+// torch loaded), so that one RCCL instance serves torch.distributed and the engine.
+struct Rccl {
+    bool ok = false;
+    ncclResult_t (*get_unique_id)(ncclUniqueId *) = nullptr;
+    ncclResult_t (*comm_init_rank)(ncclComm_t *, int, ncclUniqueId, int) = nullptr;
+    ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
+    ncclResult_t (*all_reduce)(const void *, void *, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t,
+                               hipStream_t) = nullptr;
+    const char *(*error_string)(ncclResult_t) = nullptr;
+};
+
+int rccl_load(const char *path, Rccl **out) {
+    static Rccl r;
+    static std::string err;
+    if (!r.ok) {
+        void *h = nullptr;
+        if (path && *path) h = dlopen(path, RTLD_NOW | RTLD_GLOBAL);
+        if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);
+        if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) return fail(HMMBW_E_UNSUPPORTED, std::string("cannot load RCCL: ") + dlerror());
+        r.get_unique_id = reinterpret_cast<decltype(r.get_unique_id)>(dlsym(h, "ncclGetUniqueId"));
+        r.comm_init_rank = reinterpret_cast<decltype(r.comm_init_rank)>(dlsym(h, "ncclCommInitRank"));
+        r.comm_destroy = reinterpret_cast<decltype(r.comm_destroy)>(dlsym(h, "ncclCommDestroy"));
+        r.all_reduce = reinterpret_cast<decltype(r.all_reduce)>(dlsym(h, "ncclAllReduce"));
+        r.error_string = reinterpret_cast<decltype(r.error_string)>(dlsym(h, "ncclGetErrorString"));
+        if (!r.get_unique_id || !r.comm_init_rank || !r.comm_destroy || !r.all_reduce || !r.error_string)
+            return fail(HMMBW_E_UNSUPPORTED, "RCCL library lacks the ncclGetUniqueId / ncclCommInitRank / "
+                                             "ncclCommDestroy / ncclAllReduce / ncclGetErrorString symbols");
+        r.ok = true;
+    }
+    *out = &r;
+    return HMMBW_OK;
+}
+
+int rccl_fail(const Rccl *r, ncclResult_t e, const char *what) {
+    return fail(HMMBW_E_HIP, std::string(what) + ": " + (r && r->error_string ? r->error_string(e) : "RCCL error"));
+}
+
 void resolve_topology(hmmbw_ctx *c) {
     int t = c->topo_req;
     if (c->wide) t = HMMBW_TOPOLOGY_DENSE;
@@ -521,7 +567,12 @@ int hmmbw_ctx_destroy(hmmbw_ctx *c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     else (void)hipDeviceSynchronize();
     dfree(c->d_pi); dfree(c->d_A); dfree(c->d_B); dfree(c->d_Bt); dfree(c->d_out);
-    dfree(c->d_state); dfree(c->d_hist); dfree(c->d_copies);
+    dfree(c->d_state); dfree(c->d_hist); dfree(c->d_copies); dfree(c->d_ext);
+    if (c->comm) {
+        Rccl *r = nullptr;
+        if (rccl_load(nullptr, &r) == HMMBW_OK) (void)r->comm_destroy(c->comm);
+        c->comm = nullptr;
+    }
     free_obs(c);
     for (auto e : c->ev_free) (void)hipEventDestroy(e);
     for (auto e : c->ev_pending) (void)hipEventDestroy(e);
@@ -810,7 +861,21 @@ int hmmbw_mstep(hmmbw_ctx *c, double *stats_dev, int64_t n_seq_global) {
 
 int hmmbw_iterate(hmmbw_ctx *c, int64_t n_iter) {
     if (int rc = check_ready(c, true)) return rc;
-    if (c->world != 1) return fail(HMMBW_E_STATE, "hmmbw_iterate is single-rank; use estep/all-reduce/mstep");
+    if (c->world != 1 || c->comm) {
+        // multi-rank with the native communicator: estep -> ncclAllReduce (this stream) -> mstep
+        if (!c->comm) return fail(HMMBW_E_STATE, "multi-rank hmmbw_iterate needs hmmbw_comm_init "
+                                                 "(or use estep / all-reduce / mstep)");
+        Rccl *r = nullptr;
+        if (int rc = rccl_load(nullptr, &r)) return rc;
+        for (int64_t i = 0; i < n_iter; ++i) {
+            if (int rc = hmmbw_estep(c, c->d_ext)) return rc;
+            ncclResult_t e = r->all_reduce(c->d_ext, c->d_ext, (size_t)c->stats_len(), ncclFloat64, ncclSum, c->comm,
+                                           c->stream);
+            if (e != ncclSuccess) return rccl_fail(r, e, "ncclAllReduce");
+            if (int rc = hmmbw_mstep(c, c->d_ext, c->R_global)) return rc;
+        }
+        return HMMBW_OK;
+    }
     const long long nz = (long long)c->ncopies * c->copy_len();
     for (int64_t i = 0; i < n_iter; ++i) {
         if (c->pend.on && !c->can_merge())
@@ -1034,6 +1099,46 @@ int group_launch(hmmbw_group *g, const std::vector<Plan> &plans, int n_launch, b
 }  // namespace
 
 extern "C" {
+
+int hmmbw_comm_unique_id(const char *rccl_path, void *id_out) {
+    if (!id_out) return fail(HMMBW_E_INVALID, "null argument");
+    Rccl *r = nullptr;
+    if (int rc = rccl_load(rccl_path, &r)) return rc;
+    ncclUniqueId id;
+    ncclResult_t e = r->get_unique_id(&id);
+    if (e != ncclSuccess) return rccl_fail(r, e, "ncclGetUniqueId");
+    std::memcpy(id_out, &id, sizeof(id));
+    return HMMBW_OK;
+}
+
+int hmmbw_comm_init(hmmbw_ctx *c, const char *rccl_path, const void *id, int rank, int world, int64_t n_seq_global) {
+    if (!c || !id) return fail(HMMBW_E_INVALID, "null argument");
+    if (world < 1 || rank < 0 || rank >= world) return fail(HMMBW_E_INVALID, "need 0 <= rank < world");
+    if (c->world != world || c->rank != rank) return fail(HMMBW_E_STATE, "hmmbw_set_rank first, with the same rank/world");
+    if (n_seq_global < 0) return fail(HMMBW_E_INVALID, "negative sequence count");
+    Rccl *r = nullptr;
+    if (int rc = rccl_load(rccl_path, &r)) return rc;
+    if (int rc = set_device(c)) return rc;
+    if (c->comm) {
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        (void)r->comm_destroy(c->comm);
+        c->comm = nullptr;
+    }
+    ncclUniqueId uid;
+    std::memcpy(&uid, id, sizeof(uid));
+    ncclComm_t comm = nullptr;
+    ncclResult_t e = r->comm_init_rank(&comm, world, uid, rank);
+    if (e != ncclSuccess) return rccl_fail(r, e, "ncclCommInitRank");
+    dfree(c->d_ext);
+    if (int rc = dalloc(&c->d_ext, (size_t)c->stats_len())) {
+        (void)r->comm_destroy(comm);
+        return rc;
+    }
+    HIP_TRY(hipMemset(c->d_ext, 0, sizeof(double) * (size_t)c->stats_len()));
+    c->comm = comm;
+    c->R_global = n_seq_global;
+    return HMMBW_OK;
+}
 
 int hmmbw_vq_encode(void *stream, const double *frames, int64_t n_frames, int frame_stride, int first_dim, int dims,
                     const double *centroids, int n_centroids, int32_t *symbols, double *distances) {

@@ -9,10 +9,14 @@ Multiple ranks (one process per GPU, torch.distributed over RCCL): every rank ow
 length-balanced shard of the sequences; per iteration it runs the E-step on its shard, the packed
 fp64 statistics are summed with ONE all-reduce, and every rank runs the identical M-step, so the
 parameters and the convergence decision stay replicated without a broadcast.
+With the nccl backend the engine gets its own RCCL communicator (hmmbw_comm_init) and the whole
+estep -> all-reduce -> mstep sequence is enqueued by hmmbw_iterate on the engine's stream;
+otherwise (gloo, or HMMBW_NATIVE_COMM=0) the all-reduce goes through torch.distributed.
 """
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import Callable, List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -105,7 +109,7 @@ class BaumWelchEngine:
 
     def __init__(self, n_states: int, n_symbols: int, device: Optional[int] = None, topology: str = "auto",
                  rank: int = 0, world_size: int = 1, stream: Optional[int] = None, safe_scaling: bool = False,
-                 merge_mstep: bool = True, stat_copies: int = 1):
+                 merge_mstep: bool = True, stat_copies: int = 1, group=None, native_comm: Optional[bool] = None):
         self._lib = lib()
         self.N, self.M = int(n_states), int(n_symbols)
         self.device = default_device() if device is None else int(device)
@@ -128,6 +132,12 @@ class BaumWelchEngine:
             check(self._lib.hmmbw_set_option(self._ctx, OPT_STAT_COPIES, int(stat_copies)))
         self.n_seq = 0
         self.n_seq_global = 0
+        self._group = group
+        self._native = False   # multi-rank iterations through the engine's own RCCL communicator
+        self._native_R = None
+        if native_comm is None:
+            native_comm = os.environ.get("HMMBW_NATIVE_COMM", "1") != "0"
+        self._want_native = bool(native_comm) and self.world_size > 1
 
     # -------------------------------------------------------------------------------- set-up
     def set_observations(self, observations: Sequence[np.ndarray] = None, offsets: np.ndarray = None,
@@ -140,6 +150,38 @@ class BaumWelchEngine:
         check(self._lib.hmmbw_set_observations(self._ctx, offsets.ctypes.data, symbols.ctypes.data, R))
         self.n_seq = R
         self.n_seq_global = R if n_seq_global is None else int(n_seq_global)
+        if self._want_native and self._native_R != self.n_seq_global:
+            self._native = self._init_native_comm()
+            self._native_R = self.n_seq_global if self._native else None
+
+    def _init_native_comm(self) -> bool:
+        """Collective over the ranks: give the context its own RCCL communicator (hmmbw_comm_init), so
+        multi-rank iterations run estep -> ncclAllReduce -> mstep on the engine's stream with no
+        per-iteration host hop.  Every rank first checks it can resolve RCCL; unless all can, all
+        keep the torch.distributed all-reduce path (no rank ever enters a collective alone)."""
+        import torch.distributed as dist
+        if not (dist.is_available() and dist.is_initialized()):
+            return False
+        if dist.get_backend(self._group) != "nccl":
+            return False
+        path = os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so")
+        cpath = path.encode() if os.path.exists(path) else None
+        uid = ctypes.create_string_buffer(128)
+        ok = self._lib.hmmbw_comm_unique_id(cpath, uid) == 0
+        flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=f"cuda:{self.device}")
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self._group)
+        if int(flag.item()) == 0:
+            return False
+        obj = [uid.raw]
+        src = dist.get_global_rank(self._group, 0) if self._group is not None else 0
+        dist.broadcast_object_list(obj, src=src, group=self._group, device=torch.device("cuda", self.device))
+        check(self._lib.hmmbw_comm_init(self._ctx, cpath, ctypes.c_char_p(obj[0]), self.rank, self.world_size,
+                                        self.n_seq_global))
+        return True
+
+    @property
+    def native_comm(self) -> bool:
+        return self._native
 
     def set_params(self, pi: np.ndarray, A: np.ndarray, B: np.ndarray) -> None:
         pi = np.ascontiguousarray(pi, dtype=np.float64).reshape(self.N)
@@ -172,7 +214,7 @@ class BaumWelchEngine:
 
     def enqueue_iterations(self, n: int, stats: Optional[torch.Tensor] = None, group=None) -> None:
         """Enqueue n EM iterations (asynchronous).  Multi-rank when world_size > 1."""
-        if self.world_size == 1:
+        if self.world_size == 1 or self._native:
             check(self._lib.hmmbw_iterate(self._ctx, int(n)))
             return
         import torch.distributed as dist
@@ -189,7 +231,7 @@ class BaumWelchEngine:
               group=None, max_chunk: int = 32) -> Status:
         """Run EM to the reference's stop rule; on_iteration(k, L_k, diff_k) for every iteration."""
         self.reset(epsilon, max_iterations)
-        stats = self.make_stats_buffer() if self.world_size > 1 else None
+        stats = self.make_stats_buffer() if self.world_size > 1 and not self._native else None
         reported, chunk = 0, 1
         while True:
             st, _ = self.status()

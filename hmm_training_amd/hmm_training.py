@@ -225,7 +225,7 @@ def hmm_training(observations: List[np.ndarray], N: int = 4, M: int = 256, epsil
     else:
         local = obs
 
-    engine = BaumWelchEngine(N, M, device=device, topology=topology, rank=rank, world_size=world)
+    engine = BaumWelchEngine(N, M, device=device, topology=topology, rank=rank, world_size=world, group=group)
     try:
         engine.set_observations(local, n_seq_global=len(obs))
         engine.set_params(pi0, A0, B0)

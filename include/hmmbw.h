@@ -107,10 +107,23 @@ int hmmbw_estep(hmmbw_ctx *ctx, double *stats_dev);
  * then; hmmbw_get_status / get_params / score / set_params / reset_training complete it first. */
 int hmmbw_mstep(hmmbw_ctx *ctx, double *stats_dev, int64_t n_seq_global);
 
-/* Single-rank loop: enqueue n_iter iterations of (estep, mstep) with internal statistics (the last
- * M-step stays deferred until a query, as for hmmbw_mstep).  Iterations after convergence are
- * device-side no-ops (same result as stopping, :346). */
+/* Enqueue n_iter iterations of (estep, mstep) with internal statistics (the last M-step stays
+ * deferred until a query, as for hmmbw_mstep).  Iterations after convergence are device-side no-ops
+ * (same result as stopping, :346).  Single rank, or several ranks with hmmbw_comm_init (below). */
 int hmmbw_iterate(hmmbw_ctx *ctx, int64_t n_iter);
+
+/* Native RCCL communicator for the multi-rank loop.  With it, hmmbw_iterate(ctx, n) on a context of
+ * world_size > 1 runs n iterations of {estep -> ncclAllReduce(sum) of the packed statistics on the
+ * context's stream -> mstep} with no host round trip, replacing the per-iteration
+ * torch.distributed.all_reduce hop (one RCCL all-reduce per EM iteration either way).  rccl_path:
+ * the RCCL library the process already uses (torch's librccl.so), or NULL to look it up.  Rank 0
+ * calls hmmbw_comm_unique_id and shares the 128-byte id (e.g. torch.distributed.broadcast); then
+ * every rank calls hmmbw_comm_init (collective: all ranks must call it) after hmmbw_set_rank.
+ * n_seq_global is the R of hmm_training.py:424 over all ranks.  (A 1-rank communicator is allowed:
+ * hmmbw_iterate then takes the same multi-rank sequence, which is how it is tested on one GPU.) */
+int hmmbw_comm_unique_id(const char *rccl_path, void *id_out);
+int hmmbw_comm_init(hmmbw_ctx *ctx, const char *rccl_path, const void *id, int rank, int world_size,
+                    int64_t n_seq_global);
 
 /* SYNC. Status plus the iteration records [first, first+count) (ring of 4096 entries). */
 int hmmbw_get_status(hmmbw_ctx *ctx, hmmbw_status *status, hmmbw_iter_record *records, int64_t first,

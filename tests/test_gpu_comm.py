@@ -1,0 +1,65 @@
+"""The engine's own RCCL communicator (hmmbw_comm_init): multi-rank iterations enqueued by
+hmmbw_iterate as estep -> ncclAllReduce -> mstep on the engine's stream.  On one GPU it runs with a
+1-rank communicator, which takes exactly that sequence; results must match the oracle like the
+single-rank path (hmm_training.py:342-514)."""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def gpu():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.fail("no HIP device visible: the GPU tests need an MI355X")
+
+
+def rccl_path():
+    import torch
+    p = os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so")
+    return p.encode() if os.path.exists(p) else None
+
+
+@pytest.mark.parametrize("topology,maxit", [("left_to_right", 8), ("dense", 5)])
+def test_native_comm_one_rank_matches_oracle(oracle, topology, maxit):
+    from hmm_training_amd._lib import check, lib
+    from hmm_training_amd.engine import BaumWelchEngine
+    from hmm_training_amd.hmm_training import default_initial_params
+    rng = np.random.default_rng(17)
+    N, K, R = 8, 256, 600
+    obs = [rng.integers(0, K, size=int(t)) for t in rng.integers(40, 220, size=R)]
+    pi, A, B = default_initial_params(N, K)
+    if topology == "dense":
+        A = 0.5 * A + 0.5 * rng.dirichlet(np.ones(N), size=N)
+    L = lib()
+    with BaumWelchEngine(N, K, device=0) as e:
+        check(L.hmmbw_set_rank(e._ctx, 0, 1))
+        e.set_observations(obs)
+        e.set_params(pi, A, B)
+        uid = ctypes.create_string_buffer(128)
+        check(L.hmmbw_comm_unique_id(rccl_path(), uid))
+        check(L.hmmbw_comm_init(e._ctx, rccl_path(), uid, 0, 1, R))
+        trace = []
+        st = e.train(1e-6, maxit, lambda k, Lk, d: trace.append(Lk))
+        p2, A2, B2 = e.params()
+    off = np.concatenate([[0], np.cumsum([len(o) for o in obs])]).astype(np.int64)
+    ref = oracle.hmm_training(off, np.concatenate(obs).astype(np.int64), N, K, 1e-6, maxit, pi, A, B)
+    assert st.iterations == ref.iterations
+    np.testing.assert_allclose(trace, ref.trace_L, rtol=1e-9)
+    for mine, theirs in ((A2, ref.A), (B2, ref.B), (p2, ref.pi)):
+        assert np.all(np.abs(mine - theirs) <= 1e-6 * np.abs(theirs) + 1e-15)
+
+
+def test_comm_init_rejects_bad_rank():
+    from hmm_training_amd._lib import lib
+    from hmm_training_amd.engine import BaumWelchEngine
+    L = lib()
+    with BaumWelchEngine(4, 16, device=0) as e:
+        uid = ctypes.create_string_buffer(128)
+        assert L.hmmbw_comm_unique_id(rccl_path(), uid) == 0
+        assert L.hmmbw_comm_init(e._ctx, rccl_path(), uid, 1, 2, 10) != 0  # set_rank was not called
+        assert L.hmmbw_comm_init(e._ctx, rccl_path(), uid, 3, 2, 10) != 0
