@@ -35,6 +35,7 @@ EXPORTED = (
     "hmmbw_iterate", "hmmbw_get_status", "hmmbw_get_params", "hmmbw_get_loglik", "hmmbw_score", "hmmbw_timing",
     "hmmbw_set_option", "hmmbw_group_create", "hmmbw_group_destroy", "hmmbw_group_iterate", "hmmbw_group_score",
     "hmmbw_group_timing", "hmmbw_vq_encode", "hmmbw_comm_unique_id", "hmmbw_comm_init",
+    "hmmbw_comm_probe",
 )
 OPT_SAFE_SCALING = 1
 OPT_ABLATE = 2
@@ -90,6 +91,7 @@ def _declare(lib):
         "hmmbw_vq_encode": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int,
                                            ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
                                            ctypes.c_void_p]),
+        "hmmbw_comm_probe": (ctypes.c_int, [ctypes.c_char_p]),
         "hmmbw_comm_unique_id": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_void_p]),
         "hmmbw_comm_init": (ctypes.c_int, [c_ctx, ctypes.c_char_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                                            ctypes.c_int64]),

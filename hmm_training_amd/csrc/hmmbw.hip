@@ -1100,6 +1100,11 @@ int group_launch(hmmbw_group *g, const std::vector<Plan> &plans, int n_launch, b
 
 extern "C" {
 
+int hmmbw_comm_probe(const char *rccl_path) {
+    Rccl *r = nullptr;
+    return rccl_load(rccl_path, &r);
+}
+
 int hmmbw_comm_unique_id(const char *rccl_path, void *id_out) {
     if (!id_out) return fail(HMMBW_E_INVALID, "null argument");
     Rccl *r = nullptr;

@@ -167,7 +167,9 @@ class BaumWelchEngine:
         path = os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so")
         cpath = path.encode() if os.path.exists(path) else None
         uid = ctypes.create_string_buffer(128)
-        ok = self._lib.hmmbw_comm_unique_id(cpath, uid) == 0
+        ok = self._lib.hmmbw_comm_probe(cpath) == 0
+        if ok and dist.get_rank(self._group) == 0:  # only the root creates the bootstrap id
+            ok = self._lib.hmmbw_comm_unique_id(cpath, uid) == 0
         flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=f"cuda:{self.device}")
         dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self._group)
         if int(flag.item()) == 0:

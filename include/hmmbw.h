@@ -121,6 +121,7 @@ int hmmbw_iterate(hmmbw_ctx *ctx, int64_t n_iter);
  * every rank calls hmmbw_comm_init (collective: all ranks must call it) after hmmbw_set_rank.
  * n_seq_global is the R of hmm_training.py:424 over all ranks.  (A 1-rank communicator is allowed:
  * hmmbw_iterate then takes the same multi-rank sequence, which is how it is tested on one GPU.) */
+int hmmbw_comm_probe(const char *rccl_path); /* HMMBW_OK if the RCCL entry points resolve (local check) */
 int hmmbw_comm_unique_id(const char *rccl_path, void *id_out);
 int hmmbw_comm_init(hmmbw_ctx *ctx, const char *rccl_path, const void *id, int rank, int world_size,
                     int64_t n_seq_global);
