@@ -51,6 +51,10 @@ __global__ void __launch_bounds__(NT * 64) k_estep_mfma(EArgs a) {
     double *X0 = smem;                                   // [2][NP][kXs]: z (forward) / V (backward)
     // smem + 2 * IMG: [2][NP][kXs] masked z (backward xi operand), addressed as putb / topb + 2 * IMG
     double *sRed = smem + (FWD_ONLY ? 2 : 4) * IMG;      // [NT][16] partial sums + block LL scratch
+    if constexpr (!FWD_ONLY)  // clear the next iteration's statistics (single rank: triple buffer)
+        for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < a.zero_len;
+             i += (long long)gridDim.x * blockDim.x)
+            a.zero[i] = 0.0;
     if (a.state != nullptr && a.state->done) return;    // converged: device-side no-op (:346)
     const int tid = threadIdx.x, lane = tid & 63, m = tid >> 6;
     const int s = lane & 15, g = lane >> 4;

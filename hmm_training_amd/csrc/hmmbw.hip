@@ -28,6 +28,7 @@
 //                   (max, sum exp) pair of log P_r.
 //   k_mstep / k_mstep_staged  one workgroup: L, M-step, convergence record, zero the statistics
 //                   (staged: all statistics gathered into LDS with one batch of loads).
+//   k_mstep_grid    large N x K (wide path): B re-estimated by the whole grid, the rest by workgroup 0.
 //   k_finalise  the reference's return-path normalisation (:524-541).
 #include <dlfcn.h>
 #include <rccl/rccl.h>
@@ -69,6 +70,11 @@ __global__ void __launch_bounds__(256) k_reduce_local(double *copies, int ncopie
 __global__ void __launch_bounds__(256) k_mstep(MArgs m) {
     if (carry_if_done(m)) return;
     mstep_block<false>(m);
+}
+
+__global__ void __launch_bounds__(256) k_mstep_grid(MArgs m) {
+    if (carry_if_done(m)) return;
+    mstep_grid(m);
 }
 
 // single-rank M-step with the statistics staged in dynamic LDS (copy_len doubles)
@@ -322,8 +328,12 @@ int flush_mstep(hmmbw_ctx *c) {
     c->pend.on = false;
     const MArgs m = make_margs(c, c->pend);
     const size_t staged = sizeof(double) * (size_t)c->copy_len();
+    const long long nb = (long long)c->N * c->K;
     if (m.local_lse && staged <= 64 * 1024 && c->N * c->N <= 256)
         hipLaunchKernelGGL(k_mstep_staged, dim3(1), dim3(256), staged, c->stream, m);
+    else if (nb > 8192)  // large B: the whole grid re-estimates it (one workgroup took 150 us at 64 x 1024)
+        hipLaunchKernelGGL(k_mstep_grid, dim3((unsigned)std::min<long long>((nb + 1023) / 1024, 256)), dim3(256), 0,
+                           c->stream, m);
     else
         hipLaunchKernelGGL(k_mstep, dim3(1), dim3(256), 0, c->stream, m);
     HIP_TRY(hipGetLastError());

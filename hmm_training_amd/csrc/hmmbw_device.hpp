@@ -957,6 +957,61 @@ __device__ void mstep_block(const MArgs &m) {
 
 
 
+// M-step + convergence spread over the whole grid (large N x K, e.g. the wide path's 64 x 1024 B):
+// every workgroup re-estimates its grid-stride share of B (:460-497) from the statistics summed over
+// the copies; workgroup 0 also does pi (:415-424), A (:429-455), L and the convergence record
+// (:503-514).  The statistics are only read (each E-step launch clears the buffer it will fill), so
+// no workgroup depends on another.
+__device__ __forceinline__ double peek(const MArgs &m, long long idx) {
+    double v = 0.0;
+    for (int c = 0; c < m.nsrc; ++c) v += m.src[c * m.copy_len + idx];
+    return v;
+}
+
+__device__ void mstep_grid(const MArgs &m) {
+    __shared__ double sh[16];
+    __shared__ double sL;
+    __shared__ double sGall[64];
+    const int tid = threadIdx.x;
+    const int N = m.N, K = m.K;
+    for (int i = tid; i < N; i += blockDim.x) sGall[i] = mstep_inv(peek(m, m.off_gall + i));
+    __syncthreads();
+    for (long long idx = (long long)blockIdx.x * blockDim.x + tid; idx < (long long)N * K;
+         idx += (long long)gridDim.x * blockDim.x) {
+        const int jj = (int)(idx % N), k = (int)(idx / N);  // symbol-major: coalesced reads
+        const double v = bnum_to_b(peek(m, m.off_bnum + idx), sGall[jj]);
+        m.B[(long long)jj * K + k] = v;
+        m.Bt[(long long)k * m.G + (m.bt_perm ? bt_col(jj) : jj)] = v;
+    }
+    if (blockIdx.x != 0) return;
+    if (m.local_lse) {
+        double mx, s;
+        combine_ll_pairs<false>(m.llpart, m.nblocks, sh, &mx, &s);
+        if (tid == 0) sL = (s > 0.0) ? mx + log(s) : -INFINITY;
+    } else if (tid == 0) {
+        const double *ll = m.src + m.off_ll;
+        double mx = -INFINITY;
+        for (int r = 0; r < m.world; ++r)
+            if (ll[2 * r + 1] > 0.0) mx = fmax(mx, ll[2 * r]);
+        double s = 0.0;
+        if (mx != -INFINITY)
+            for (int r = 0; r < m.world; ++r)
+                if (ll[2 * r + 1] > 0.0) s += ll[2 * r + 1] * exp(ll[2 * r] - mx);
+        sL = (s > 0.0) ? mx + log(s) : -INFINITY;
+    }
+    for (int i = tid; i < N; i += blockDim.x) {
+        const double pn = peek(m, i);
+        m.pi[i] = pn > 0.0 ? pn / (double)m.R_global : 0.0;
+    }
+    for (int idx = tid; idx < N * N; idx += blockDim.x) {
+        const double den = peek(m, m.off_gex + idx / N);
+        const double num = peek(m, m.off_S + idx);
+        m.A[idx] = (den > 0.0 && num > 0.0) ? num / den : 0.0;
+    }
+    __syncthreads();
+    if (tid == 0) record_iteration(m, *m.state, sL);
+}
+
 // merge (max, sum exp) pairs: online log-sum-exp
 __device__ __forceinline__ void ll_merge(double &M, double &S, double m2, double s2) {
     if (!(s2 > 0.0)) return;

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Copy the summaries of one tools/profile_r1.sh run (gpurun_out/prof_<tag>) into profiles/<dest>/ and
+# Copy the summaries of one tools/profile_all.sh run (gpurun_out/prof_<tag>) into profiles/<dest>/ and
 # rebuild the per-launch traffic JSONs bench.py reads.   bash tools/collect_profiles.sh <tag> <dest>
 set -euo pipefail
 TAG=$1; DEST=$2
@@ -17,5 +17,11 @@ for TOPO in left_to_right dense; do
     --calib-fetch "profiles/$DEST/pmc_calib_FETCH_SIZE.csv" --calib-write "profiles/$DEST/pmc_calib_WRITE_SIZE.csv" \
     --kernel k_estep_small --config-key "R10000_T200_N8_K256_$TOPO" --out "profiles/$DEST/traffic_${TOPO}_cfg3.json"
 done
+for W in cfg5 cfg2 vq; do
+  cp "$SRC/trace_$W/run_kernel_stats.csv" "profiles/$DEST/kernel_stats_$W.csv"
+done
 grep -h '"metric"' "$SRC/bench_full.log" > "profiles/$DEST/bench_lr_cfg3.json"
 grep -h '"metric"' "$SRC/bench_dense.log" > "profiles/$DEST/bench_dense_cfg3.json"
+grep -h '"metric"' "$SRC/bench_cfg5.log" > "profiles/$DEST/bench_cfg5.json"
+grep -h '"workload"' "$SRC/bench_cfg2_full.log" > "profiles/$DEST/bench_cfg2_grouped.json"
+grep -h '"kernel"' "$SRC/bench_vq.log" > "profiles/$DEST/bench_vq.json"
