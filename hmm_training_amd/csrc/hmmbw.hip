@@ -178,7 +178,7 @@ struct hmmbw_ctx {
     int scur = 0;
     double *d_hist = nullptr;
     double *d_copies = nullptr;   // [3][ncopies][copy_len] E-step accumulators (iteration e uses e % 3)
-    int ncopies = 1;
+    int ncopies = 2;              // HMMBW_OPT_STAT_COPIES default: halves the flush atomics per address (measured -3 %)
     bool merge_mstep = true;      // run each M-step in the prologue of the next E-step launch
     bool armed = false;
     long long e_count = 0;        // E-step launches since the statistics were last cleared

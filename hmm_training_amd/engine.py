@@ -109,7 +109,7 @@ class BaumWelchEngine:
 
     def __init__(self, n_states: int, n_symbols: int, device: Optional[int] = None, topology: str = "auto",
                  rank: int = 0, world_size: int = 1, stream: Optional[int] = None, safe_scaling: bool = False,
-                 merge_mstep: bool = True, stat_copies: int = 1, group=None, native_comm: Optional[bool] = None):
+                 merge_mstep: bool = True, stat_copies: Optional[int] = None, group=None, native_comm: Optional[bool] = None):
         self._lib = lib()
         self.N, self.M = int(n_states), int(n_symbols)
         self.device = default_device() if device is None else int(device)
@@ -128,7 +128,7 @@ class BaumWelchEngine:
             check(self._lib.hmmbw_set_option(self._ctx, OPT_SAFE_SCALING, 1))
         if not merge_mstep:
             check(self._lib.hmmbw_set_option(self._ctx, OPT_MERGE_MSTEP, 0))
-        if stat_copies != 1:
+        if stat_copies is not None:  # None: the library default (2)
             check(self._lib.hmmbw_set_option(self._ctx, OPT_STAT_COPIES, int(stat_copies)))
         self.n_seq = 0
         self.n_seq_global = 0

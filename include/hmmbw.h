@@ -150,7 +150,7 @@ int hmmbw_score(hmmbw_ctx *ctx, double *out);
  * statistics flush, bit 1 skips its backward sweep. */
 #define HMMBW_OPT_ABLATE 2
 /* Number of statistics accumulator copies the E-step's workgroups spread their atomics over
- * (workgroup b adds into copy b % n; default 1). */
+ * (workgroup b adds into copy b % n; default 2). */
 #define HMMBW_OPT_STAT_COPIES 3
 /* 1 (default): every M-step runs in the prologue of the next E-step launch, computed redundantly by
  * each workgroup straight into its LDS tables (when the emission tables fit LDS); 0: a separate
