@@ -115,8 +115,9 @@ __global__ void __launch_bounds__(NT * 64) k_estep_mfma(EArgs a) {
     // ---------------- forward (hmm_training.py:357-368; hmm_testing.py:70-92) ----------------
     f64x4 z = {0.0, 0.0, 0.0, 0.0};
     int C = 0;
-    f64x4 bring[2];  // b(o_t) in slot t % 2, loaded one step ahead
-    bring[0] = emis(sym_of(loadpack(0), 0));
+    // b(o_t) in slot t % 4, loaded kLook steps ahead; symbol packs one chunk ahead of their use
+    constexpr int kLook = 3;
+    f64x4 bring[4];
     auto fstep = [&](int t, const f64x4 &b, auto MASK_) {
         constexpr bool MASK = decltype(MASK_)::value;
         f64x4 x;
@@ -169,16 +170,21 @@ __global__ void __launch_bounds__(NT * 64) k_estep_mfma(EArgs a) {
         if (!(a.ablate & 16)) __syncthreads();
     };
     auto forward = [&](auto MASK_) {
+        uint4 p0 = loadpack(0), p1 = loadpack(nch > 1 ? 1 : 0);  // chunks c and c + 1
+#pragma unroll
+        for (int i = 0; i < kLook; ++i) bring[i] = emis(sym_of(p0, i));
         for (int c = 0; c < nch; ++c) {
-            const uint4 pc = loadpack(c);
-            const uint4 pn = loadpack(c + 1 < nch ? c + 1 : c);
+            const uint4 p2 = loadpack(c + 2 < nch ? c + 2 : nch - 1);
 #pragma unroll
             for (int k = 0; k < kChunk; ++k) {
                 const int t = c * kChunk + k;
-                bring[(k + 1) & 1] = emis(k + 1 < kChunk ? sym_of(pc, k + 1) : sym_of(pn, 0));  // b(o_{t+1})
+                // b(o_{t + kLook}) into the slot step t - 1 has consumed
+                bring[(k + kLook) & 3] = emis(k + kLook < kChunk ? sym_of(p0, k + kLook) : sym_of(p1, k + kLook - kChunk));
                 if (t >= Tw) continue;  // tile-uniform
-                fstep(t, bring[k & 1], MASK_);
+                fstep(t, bring[k & 3], MASK_);
             }
+            p0 = p1;
+            p1 = p2;
         }
     };
     if (full) forward(std::false_type{});
@@ -229,9 +235,9 @@ __global__ void __launch_bounds__(NT * 64) k_estep_mfma(EArgs a) {
         f64x4 S[NT];
 #pragma unroll
         for (int mm = 0; mm < NT; ++mm) S[mm] = f64x4{0.0, 0.0, 0.0, 0.0};
-        // ring (slot t % 2, loaded one step ahead): alpha_hat_t, b(o_{t+1}), s_{t+1}
-        f64x4 zring[2], bring1[2];
-        int sring[2];
+        // ring (slot t % 4, loaded kLook steps ahead): alpha_hat_t, b(o_{t+1}), s_{t+1}
+        f64x4 zring[4], bring1[4];
+        int sring[4];
         auto ldz = [&](int t) -> f64x4 {
             f64x4 v;
             if (a.ablate & 8) return f64x4{0.5, 0.5, 0.5, 0.5};
@@ -295,23 +301,34 @@ __global__ void __launch_bounds__(NT * 64) k_estep_mfma(EArgs a) {
             }
         };
         auto backward = [&](auto MASK_) {
-            zring[1] = f64x4{0.0, 0.0, 0.0, 0.0};
-            bring1[1] = zring[1];
-            sring[1] = 0;
+            const int ttop = nch * kChunk;  // steps ttop - 1 .. 0 are visited (those > Tw - 2 skip)
+            uint4 pc = loadpack(nch - 1);   // chunk c; chunk c - 1's pack is loaded at the top of chunk c
+            // inputs of the first kLook visited steps s = ttop - 1 - i (o_{s+1} = o_ttop does not exist)
+#pragma unroll
+            for (int i = 0; i < kLook; ++i) {
+                const int s0 = ttop - 1 - i;
+                const int sl = s0 & 3;
+                zring[sl] = s0 >= 0 ? ldz(s0) : f64x4{0.0, 0.0, 0.0, 0.0};
+                bring1[sl] = (i >= 1 && s0 >= 0) ? emis(sym_of(pc, kChunk - i)) : f64x4{0.0, 0.0, 0.0, 0.0};
+                sring[sl] = (i >= 1 && s0 >= 0) ? ew[(s0 + 1) * kTileSeqs] : 0;
+            }
             for (int c = nch - 1; c >= 0; --c) {
-                const uint4 pc = loadpack(c);
+                const uint4 pp = loadpack(c >= 1 ? c - 1 : 0);
 #pragma unroll
                 for (int k = kChunk - 1; k >= 0; --k) {
                     const int t = c * kChunk + k;
-                    // step t-1's inputs into the slot step t+1 has consumed
-                    if (t >= 1) {
-                        zring[(k + 1) & 1] = ldz(t - 1);
-                        bring1[(k + 1) & 1] = emis(sym_of(pc, k));  // b(o_t)
-                        sring[(k + 1) & 1] = ew[t * kTileSeqs];     // s_t
+                    // step t - kLook's inputs into the slot step t + 1 has consumed
+                    const int s0 = t - kLook;
+                    if (s0 >= 0) {
+                        const int q = k - kLook + 1;  // o_{s0 + 1}: index q of chunk c, or of chunk c - 1
+                        zring[(k - kLook) & 3] = ldz(s0);
+                        bring1[(k - kLook) & 3] = emis(q >= 0 ? sym_of(pc, q) : sym_of(pp, q + kChunk));
+                        sring[(k - kLook) & 3] = ew[(s0 + 1) * kTileSeqs];
                     }
                     if (t > Tw - 2) continue;  // tile-uniform; gamma_{T-1} is done above
-                    bstep(t, zring[k & 1], bring1[k & 1], sring[k & 1], MASK_);
+                    bstep(t, zring[k & 3], bring1[k & 3], sring[k & 3], MASK_);
                 }
+                pc = pp;
             }
         };
         if (full) backward(std::false_type{});
