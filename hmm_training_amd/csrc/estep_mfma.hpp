@@ -38,14 +38,27 @@ namespace hmmbw {
 typedef double f64x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kTileSeqs = 16;  // sequences per tile = MFMA columns
+
+// Profiling ablations of the inner loops (results wrong by construction) exist only in a diagnostics
+// build (-DHMMBW_WIDE_ABLATE): a runtime test inside the step loops costs the release build its
+// counted vmcnt waits (the join points after such branches drain every prefetch with vmcnt(0)).
+#ifdef HMMBW_WIDE_ABLATE
+#define WIDE_ABL(a, bit) (((a).ablate & (bit)) != 0)
+#else
+#define WIDE_ABL(a, bit) false
+#endif
 constexpr int kXs = 17;        // LDS row stride (doubles) of a [state][16 sequences] image
+
+// every helper lambda of the kernel is force-inlined: a lambda left out of line keeps the f64x4
+// state it captures by reference (beta, gamma sums) in scratch memory
+#define HMMBW_AI __attribute__((always_inline))
 
 __device__ __forceinline__ f64x4 mfma_f64(double a, double b, f64x4 c) {
     return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
 }
 
 template <int NT, bool FWD_ONLY>
-__global__ void __launch_bounds__(NT * 64) k_estep_mfma(EArgs a) {
+__global__ void __launch_bounds__(NT * 64, 2) k_estep_mfma(EArgs a) {  // 2 waves per SIMD: <= 256 VGPRs
     constexpr int NP = 16 * NT, KB = 4 * NT, IMG = NP * kXs;
     extern __shared__ double smem[];
     double *X0 = smem;                                   // [2][NP][kXs]: z (forward) / V (backward)
@@ -72,16 +85,16 @@ __global__ void __launch_bounds__(NT * 64) k_estep_mfma(EArgs a) {
     const int col0 = 16 * m + 4 * g;  // this lane's 4 emission columns (bt_col order)
     // gamma row of position (t, s): gw + t * 16 * NP, this lane's 4 columns
     double *gw = a.gam + (FWD_ONLY ? 0 : a.L.wave_ckoff[tile]) + (long long)s * NP + col0;
-    auto putg = [&](int t, const f64x4 &v) {
+    auto putg = [&](int t, const f64x4 &v) HMMBW_AI {
         double2 *q = reinterpret_cast<double2 *>(gw + (long long)t * kTileSeqs * NP);
         q[0] = double2{v[0], v[1]};
         q[1] = double2{v[2], v[3]};
     };
 
-    auto loadpack = [&](int c) -> uint4 {
+    auto loadpack = [&](int c) HMMBW_AI -> uint4 {
         return *reinterpret_cast<const uint4 *>(symw + (long long)c * kTileSeqs * kChunk);
     };
-    auto emis = [&](int o) -> f64x4 {  // b_j(o) for j = 16m + g + 4r, r = 0..3
+    auto emis = [&](int o) HMMBW_AI -> f64x4 {  // b_j(o) for j = 16m + g + 4r, r = 0..3
         const double2 *p = reinterpret_cast<const double2 *>(a.Bt + (long long)o * NP + col0);
         const double2 lo = p[0], hi = p[1];
         return f64x4{lo.x, lo.y, hi.x, hi.y};
@@ -89,15 +102,15 @@ __global__ void __launch_bounds__(NT * 64) k_estep_mfma(EArgs a) {
     // this wave's block of a [state][16] LDS image (C/D form), the B operand of k-block kb, and the
     // transposed read [state 16mm + (lane & 15)][sequence 4kk + (lane >> 4)] (the xi operands)
     double *const putb = X0 + (16 * m + g) * kXs + s;
-    auto put = [&](double *base, int p, const f64x4 &v) {
+    auto put = [&](double *base, int p, const f64x4 &v) HMMBW_AI {
 #pragma unroll
         for (int r = 0; r < 4; ++r) base[p * IMG + 4 * r * kXs] = v[r];
     };
     const double *const bopb = X0 + g * kXs + s;
     const double *const topb = X0 + (lane & 15) * kXs + (lane >> 4);
-    auto bexp = [](double x) -> int { return (int)__builtin_amdgcn_ubfe((unsigned)__double2hiint(x), 20, 11); };
+    auto bexp = [](double x) HMMBW_AI -> int { return (int)__builtin_amdgcn_ubfe((unsigned)__double2hiint(x), 20, 11); };
     // sum over the 16 sequences of a 16-lane row
-    auto rowsum = [](double x) -> double {
+    auto rowsum = [](double x) HMMBW_AI -> double {
 #pragma unroll
         for (int q = 1; q < kTileSeqs; q <<= 1) x += __shfl_xor(x, q);
         return x;
@@ -118,7 +131,7 @@ __global__ void __launch_bounds__(NT * 64) k_estep_mfma(EArgs a) {
     // b(o_t) in slot t % 4, loaded kLook steps ahead; symbol packs one chunk ahead of their use
     constexpr int kLook = 3;
     f64x4 bring[4];
-    auto fstep = [&](int t, const f64x4 &b, auto MASK_) {
+    auto fstep = [&](int t, const f64x4 &b, auto MASK_) HMMBW_AI {
         constexpr bool MASK = decltype(MASK_)::value;
         f64x4 x;
         int sc = 0;
@@ -161,15 +174,15 @@ __global__ void __launch_bounds__(NT * 64) k_estep_mfma(EArgs a) {
         C += sc;
         put(putb, t & 1, z);
         if constexpr (!FWD_ONLY) {
-            if (!(a.ablate & 8)) {
+            if (!WIDE_ABL(a, 8)) {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) ckw[((long long)t * NT * 4 + r) * 64] = z[r];
             }
             if (m == 0 && g == 0) ew[t * kTileSeqs] = sc;
         }
-        if (!(a.ablate & 16)) __syncthreads();
+        if (!WIDE_ABL(a, 16)) __syncthreads();
     };
-    auto forward = [&](auto MASK_) {
+    auto forward = [&](auto MASK_) HMMBW_AI {
         uint4 p0 = loadpack(0), p1 = loadpack(nch > 1 ? 1 : 0);  // chunks c and c + 1
 #pragma unroll
         for (int i = 0; i < kLook; ++i) bring[i] = emis(sym_of(p0, i));
@@ -213,7 +226,7 @@ __global__ void __launch_bounds__(NT * 64) k_estep_mfma(EArgs a) {
             f64x4 gT;
 #pragma unroll
             for (int r = 0; r < 4; ++r) gT[r] = z[r] * inv_p;
-            if (T > 0 && !(a.ablate & 4)) putg(T - 1, gT);
+            if (T > 0 && !WIDE_ABL(a, 4)) putg(T - 1, gT);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int j = 16 * m + g + 4 * r;
@@ -231,22 +244,23 @@ __global__ void __launch_bounds__(NT * 64) k_estep_mfma(EArgs a) {
             aop[kb] = (i < N && jj < N) ? a.A[i * N + jj] : 0.0;
         }
         f64x4 beta = {inv_p, inv_p, inv_p, inv_p};
-        f64x4 gex = {0.0, 0.0, 0.0, 0.0};
+        double gex[4] = {0.0, 0.0, 0.0, 0.0};  // plain array: an f64x4 with element-wise updates stays in scratch
         f64x4 S[NT];
 #pragma unroll
         for (int mm = 0; mm < NT; ++mm) S[mm] = f64x4{0.0, 0.0, 0.0, 0.0};
-        // ring (slot t % 4, loaded kLook steps ahead): alpha_hat_t, b(o_{t+1}), s_{t+1}
-        f64x4 zring[4], bring1[4];
-        int sring[4];
-        auto ldz = [&](int t) -> f64x4 {
+        // rings: alpha_hat_t (HBM) in slot t % 4, loaded kLook steps ahead; b(o_{t+1}) (L2-resident
+        // table) and s_{t+1} in slot t % 2, loaded one step ahead (fewer VGPRs: two waves per SIMD)
+        f64x4 zring[4], bring1[2];
+        int sring[2];
+        auto ldz = [&](int t) HMMBW_AI -> f64x4 {
             f64x4 v;
-            if (a.ablate & 8) return f64x4{0.5, 0.5, 0.5, 0.5};
+            if (WIDE_ABL(a, 8)) return f64x4{0.5, 0.5, 0.5, 0.5};
 #pragma unroll
             for (int r = 0; r < 4; ++r) v[r] = ckw[((long long)t * NT * 4 + r) * 64];
             return v;
         };
         // one regular step t <= Tw - 2 (MASK: per-sequence t <= T - 2 in ragged tiles)
-        auto bstep = [&](int t, const f64x4 &zt, const f64x4 &b1, int s1, auto MASK_) {
+        auto bstep = [&](int t, const f64x4 &zt, const f64x4 &b1, int s1, auto MASK_) HMMBW_AI {
             constexpr bool MASK = decltype(MASK_)::value;
             const bool reg = !MASK || t <= T - 2;
             f64x4 v, zs;
@@ -264,7 +278,7 @@ __global__ void __launch_bounds__(NT * 64) k_estep_mfma(EArgs a) {
             const int p = t & 1;
             put(putb, p, v);
             put(putb + 2 * IMG, p, zs);
-            if (!(a.ablate & 16)) __syncthreads();
+            if (!WIDE_ABL(a, 16)) __syncthreads();
             // beta_hat_t = A v (:163-199), this wave's 16 rows
             const double *vsrc = bopb + p * IMG;
             f64x4 acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
@@ -290,7 +304,7 @@ __global__ void __launch_bounds__(NT * 64) k_estep_mfma(EArgs a) {
                 else beta[r] = bn;
                 gex[r] += gm[r];
             }
-            if ((!MASK || reg) && !(a.ablate & 4)) putg(t, gm);  // B numerator row (:474-485)
+            if ((!MASK || reg) && !WIDE_ABL(a, 4)) putg(t, gm);  // B numerator row (:474-485)
             if (t == 0) {  // pi_num (:415-420): gamma_0 summed over the tile's sequences
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
@@ -300,33 +314,30 @@ __global__ void __launch_bounds__(NT * 64) k_estep_mfma(EArgs a) {
                 }
             }
         };
-        auto backward = [&](auto MASK_) {
+        auto backward = [&](auto MASK_) HMMBW_AI {
             const int ttop = nch * kChunk;  // steps ttop - 1 .. 0 are visited (those > Tw - 2 skip)
             uint4 pc = loadpack(nch - 1);   // chunk c; chunk c - 1's pack is loaded at the top of chunk c
-            // inputs of the first kLook visited steps s = ttop - 1 - i (o_{s+1} = o_ttop does not exist)
+            // alpha_hat of the first kLook visited steps s = ttop - 1 - i; step ttop - 1 has no o_{s+1}
 #pragma unroll
             for (int i = 0; i < kLook; ++i) {
                 const int s0 = ttop - 1 - i;
-                const int sl = s0 & 3;
-                zring[sl] = s0 >= 0 ? ldz(s0) : f64x4{0.0, 0.0, 0.0, 0.0};
-                bring1[sl] = (i >= 1 && s0 >= 0) ? emis(sym_of(pc, kChunk - i)) : f64x4{0.0, 0.0, 0.0, 0.0};
-                sring[sl] = (i >= 1 && s0 >= 0) ? ew[(s0 + 1) * kTileSeqs] : 0;
+                zring[s0 & 3] = s0 >= 0 ? ldz(s0) : f64x4{0.0, 0.0, 0.0, 0.0};
             }
+            bring1[1] = f64x4{0.0, 0.0, 0.0, 0.0};
+            sring[1] = 0;
             for (int c = nch - 1; c >= 0; --c) {
                 const uint4 pp = loadpack(c >= 1 ? c - 1 : 0);
 #pragma unroll
                 for (int k = kChunk - 1; k >= 0; --k) {
                     const int t = c * kChunk + k;
-                    // step t - kLook's inputs into the slot step t + 1 has consumed
-                    const int s0 = t - kLook;
-                    if (s0 >= 0) {
-                        const int q = k - kLook + 1;  // o_{s0 + 1}: index q of chunk c, or of chunk c - 1
-                        zring[(k - kLook) & 3] = ldz(s0);
-                        bring1[(k - kLook) & 3] = emis(q >= 0 ? sym_of(pc, q) : sym_of(pp, q + kChunk));
-                        sring[(k - kLook) & 3] = ew[(s0 + 1) * kTileSeqs];
+                    // alpha_hat_{t - kLook}, b(o_t) and s_t into the slots step t + 1 has consumed
+                    if (t - kLook >= 0) zring[(k - kLook) & 3] = ldz(t - kLook);
+                    if (t >= 1) {
+                        bring1[(k + 1) & 1] = emis(sym_of(pc, k));  // b(o_t), consumed by step t - 1
+                        sring[(k + 1) & 1] = ew[t * kTileSeqs];     // s_t
                     }
                     if (t > Tw - 2) continue;  // tile-uniform; gamma_{T-1} is done above
-                    bstep(t, zring[k & 3], bring1[k & 3], sring[k & 3], MASK_);
+                    bstep(t, zring[k & 3], bring1[k & 1], sring[k & 1], MASK_);
                 }
                 pc = pp;
             }
