@@ -330,12 +330,14 @@ __global__ void __launch_bounds__(NT * 64, 2) k_estep_mfma(EArgs a) {  // 2 wave
 #pragma unroll
                 for (int k = kChunk - 1; k >= 0; --k) {
                     const int t = c * kChunk + k;
-                    // alpha_hat_{t - kLook}, b(o_t) and s_t into the slots step t + 1 has consumed
-                    if (t - kLook >= 0) zring[(k - kLook) & 3] = ldz(t - kLook);
+                    // b(o_t), s_t and alpha_hat_{t - kLook} into the slots step t + 1 has consumed; the
+                    // one-step-ahead loads go first so that waiting for them (in-order vmcnt) leaves
+                    // the deeper alpha_hat prefetch in flight
                     if (t >= 1) {
                         bring1[(k + 1) & 1] = emis(sym_of(pc, k));  // b(o_t), consumed by step t - 1
                         sring[(k + 1) & 1] = ew[t * kTileSeqs];     // s_t
                     }
+                    if (t - kLook >= 0) zring[(k - kLook) & 3] = ldz(t - kLook);
                     if (t > Tw - 2) continue;  // tile-uniform; gamma_{T-1} is done above
                     bstep(t, zring[k & 3], bring1[k & 1], sring[k & 1], MASK_);
                 }
