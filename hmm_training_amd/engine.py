@@ -177,9 +177,12 @@ class BaumWelchEngine:
         obj = [uid.raw]
         src = dist.get_global_rank(self._group, 0) if self._group is not None else 0
         dist.broadcast_object_list(obj, src=src, group=self._group, device=torch.device("cuda", self.device))
-        check(self._lib.hmmbw_comm_init(self._ctx, cpath, ctypes.c_char_p(obj[0]), self.rank, self.world_size,
-                                        self.n_seq_global))
-        return True
+        rc = self._lib.hmmbw_comm_init(self._ctx, cpath, ctypes.c_char_p(obj[0]), self.rank, self.world_size,
+                                       self.n_seq_global)
+        # second agreement: the engine communicator is used only if every rank created it
+        flag = torch.tensor([1 if rc == 0 else 0], dtype=torch.int32, device=f"cuda:{self.device}")
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self._group)
+        return int(flag.item()) == 1
 
     @property
     def native_comm(self) -> bool:
