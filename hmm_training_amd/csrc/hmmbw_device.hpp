@@ -958,9 +958,9 @@ __device__ void mstep_block(const MArgs &m) {
 
 
 // M-step + convergence spread over the whole grid (large N x K, e.g. the wide path's 64 x 1024 B):
-// every workgroup re-estimates its grid-stride share of B (:460-497) from the statistics summed over
-// the copies; workgroup 0 also does pi (:415-424), A (:429-455), L and the convergence record
-// (:503-514).  The statistics are only read (each E-step launch clears the buffer it will fill), so
+// every workgroup re-estimates its grid-stride share of B (:460-497) and A (:429-455) from the
+// statistics summed over the copies; workgroup 0 also does pi (:415-424), L and the convergence
+// record (:503-514).  The statistics are only read (each E-step launch clears the buffer it will fill), so
 // no workgroup depends on another.
 __device__ __forceinline__ double peek(const MArgs &m, long long idx) {
     double v = 0.0;
@@ -983,6 +983,12 @@ __device__ void mstep_grid(const MArgs &m) {
         m.B[(long long)jj * K + k] = v;
         m.Bt[(long long)k * m.G + (m.bt_perm ? bt_col(jj) : jj)] = v;
     }
+    for (long long idx = (long long)blockIdx.x * blockDim.x + tid; idx < (long long)N * N;
+         idx += (long long)gridDim.x * blockDim.x) {  // A (:429-455)
+        const double den = peek(m, m.off_gex + idx / N);
+        const double num = peek(m, m.off_S + idx);
+        m.A[idx] = (den > 0.0 && num > 0.0) ? num / den : 0.0;
+    }
     if (blockIdx.x != 0) return;
     if (m.local_lse) {
         double mx, s;
@@ -1002,11 +1008,6 @@ __device__ void mstep_grid(const MArgs &m) {
     for (int i = tid; i < N; i += blockDim.x) {
         const double pn = peek(m, i);
         m.pi[i] = pn > 0.0 ? pn / (double)m.R_global : 0.0;
-    }
-    for (int idx = tid; idx < N * N; idx += blockDim.x) {
-        const double den = peek(m, m.off_gex + idx / N);
-        const double num = peek(m, m.off_S + idx);
-        m.A[idx] = (den > 0.0 && num > 0.0) ? num / den : 0.0;
     }
     __syncthreads();
     if (tid == 0) record_iteration(m, *m.state, sL);
