@@ -264,7 +264,7 @@ __device__ void block_ll_partial(double lp, bool valid, double *sh, double *out)
 //   gamma_t(i) = z_t(i) beta_hat_t(i),  xi_t(i,j) = a_ij z_t(i) v_j  (accumulated as S_ij = xi/a_ij).
 // gamma is scattered into the per-workgroup LDS histogram B_num[o_t][j] (ds_add_f64).
 // ---------------------------------------------------------------------------------------------
-template <int N, int G, int GP, bool HIST, bool PT>
+template <int N, int G, int GP, bool HIST, bool PT, int BLK = kBlock>
 __device__ bool merged_mstep(const EArgs &a, double *sBt, double2 *sBP, double *sBn, double *sPA, long long bid);
 
 // Body of the small-N E-step / scorer for workgroup `bid` of the `nblk` workgroups that cover one
@@ -1128,11 +1128,11 @@ __device__ __forceinline__ double wave_max(double x) {
     return fmax(x, __shfl_xor(x, 32));
 }
 
-template <int N, int G, int GP, bool HIST, bool PT>
+template <int N, int G, int GP, bool HIST, bool PT, int BLK>
 __device__ bool merged_mstep(const EArgs &a, double *sBt, double2 *sBP, double *sBn, double *sPA, long long bid) {
     constexpr int NSM = N + N * N + 2 * N;  // pi_num, xi, gamma_den_excl, gamma_den_all
-    constexpr int NW = kBlock / 64;
-    constexpr int SB = kMergedMaxStats / kBlock;
+    constexpr int NW = BLK / 64;
+    constexpr int SB = kMergedMaxStats / BLK;
     constexpr int PB = 2;                   // log-likelihood pairs per thread per pass
     __shared__ double sSm[NSM];
     __shared__ double sMx[NW], sSum[NW];
@@ -1145,14 +1145,14 @@ __device__ bool merged_mstep(const EArgs &a, double *sBt, double2 *sBP, double *
     double v[SB];
 #pragma unroll
     for (int q = 0; q < SB; ++q) {
-        const long long idx = (long long)q * kBlock + tid;
+        const long long idx = (long long)q * BLK + tid;
         v[q] = m.src[idx < len ? idx : len - 1];
     }
     for (int c = 1; c < m.nsrc; ++c) {
         double x[SB];
 #pragma unroll
         for (int q = 0; q < SB; ++q) {
-            const long long idx = (long long)q * kBlock + tid;
+            const long long idx = (long long)q * BLK + tid;
             x[q] = m.src[c * len + (idx < len ? idx : len - 1)];
         }
 #pragma unroll
@@ -1162,7 +1162,7 @@ __device__ bool merged_mstep(const EArgs &a, double *sBt, double2 *sBP, double *
     double pm[PB], ps[PB];
 #pragma unroll
     for (int q = 0; q < PB; ++q) {
-        const long long r = (long long)q * kBlock + tid;
+        const long long r = (long long)q * BLK + tid;
         const long long rc = r < nb ? r : nb - 1;
         pm[q] = m.llpart[2 * rc];
         ps[q] = m.llpart[2 * rc + 1];
@@ -1182,16 +1182,16 @@ __device__ bool merged_mstep(const EArgs &a, double *sBt, double2 *sBP, double *
     double mx = -INFINITY;
 #pragma unroll
     for (int q = 0; q < PB; ++q) {
-        const bool ok = (long long)q * kBlock + tid < nb && ps[q] > 0.0;
+        const bool ok = (long long)q * BLK + tid < nb && ps[q] > 0.0;
         mx = ok ? fmax(mx, pm[q]) : mx;
     }
-    for (long long r = (long long)PB * kBlock + tid; r < nb; r += kBlock)  // > 512 workgroups
+    for (long long r = (long long)PB * BLK + tid; r < nb; r += BLK)  // > 512 workgroups
         if (m.llpart[2 * r + 1] > 0.0) mx = fmax(mx, m.llpart[2 * r]);
     mx = wave_max(mx);
     if (lane == 0) sMx[wv] = mx;
 #pragma unroll
     for (int q = 0; q < SB; ++q) {
-        const int idx = q * kBlock + tid;
+        const int idx = q * BLK + tid;
         if (idx < NSM) sSm[idx] = (idx < len) ? v[q] : 0.0;
     }
     if (tid == 0) sIn = in;
@@ -1208,10 +1208,10 @@ __device__ bool merged_mstep(const EArgs &a, double *sBt, double2 *sBP, double *
     if (Mb != -INFINITY) {
 #pragma unroll
         for (int q = 0; q < PB; ++q) {
-            const bool ok = (long long)q * kBlock + tid < nb && ps[q] > 0.0;
+            const bool ok = (long long)q * BLK + tid < nb && ps[q] > 0.0;
             sum += ok ? ps[q] * exp(pm[q] - Mb) : 0.0;
         }
-        for (long long r = (long long)PB * kBlock + tid; r < nb; r += kBlock)
+        for (long long r = (long long)PB * BLK + tid; r < nb; r += BLK)
             if (m.llpart[2 * r + 1] > 0.0) sum += m.llpart[2 * r + 1] * exp(m.llpart[2 * r] - Mb);
     }
     sum = gsum<64>(sum);
@@ -1225,11 +1225,11 @@ __device__ bool merged_mstep(const EArgs &a, double *sBt, double2 *sBP, double *
         sPA[G + tid] = (den > 0.0 && num > 0.0) ? num / den : 0.0;
     }
     // B (:460-497) from the registers straight into the emission table (and HBM, workgroup 0).
-    // Element e = q * kBlock + tid - NSM is symbol e / N, state e % N; with N | kBlock the state (and
+    // Element e = q * BLK + tid - NSM is symbol e / N, state e % N; with N | BLK the state (and
     // so the denominator) is the same for every q of a thread: one reciprocal per thread.
     const bool w0 = bid == 0;
     const int e0 = tid - NSM;
-    constexpr bool kSameState = (kBlock % N) == 0;
+    constexpr bool kSameState = (BLK % N) == 0;
     const int jj0 = ((e0 % N) + N) % N;
     const double inv0 = kSameState ? mstep_inv(sSm[N + N * N + N + jj0]) : 0.0;
     // PT: a_jj and a_{j-1,j} of the element's state, the same arithmetic as sPA's A (:429-455)
@@ -1246,7 +1246,7 @@ __device__ bool merged_mstep(const EArgs &a, double *sBt, double2 *sBP, double *
     double bval[SB];
 #pragma unroll
     for (int q = 0; q < SB; ++q) {
-        const int e = q * kBlock + e0;
+        const int e = q * BLK + e0;
         const int jj = kSameState ? jj0 : ((e % N) + N) % N;
         const double inv = kSameState ? inv0 : mstep_inv(sSm[N + N * N + N + jj]);
         bval[q] = bnum_to_b(v[q], inv);
@@ -1262,7 +1262,7 @@ __device__ bool merged_mstep(const EArgs &a, double *sBt, double2 *sBP, double *
     if (w0) {
 #pragma unroll
         for (int q = 0; q < SB; ++q) {
-            const int e = q * kBlock + e0;
+            const int e = q * BLK + e0;
             if (e >= 0 && e < K * N) {
                 const int k = e / N, jj = e - k * N;
                 m.B[(long long)jj * K + k] = bval[q];
@@ -1271,7 +1271,7 @@ __device__ bool merged_mstep(const EArgs &a, double *sBt, double2 *sBP, double *
         }
     }
     // zero the pad columns [N, GP) of every row and the pad row K; clear the histogram
-    for (int i = tid; i < (K + 1) * (GP - N); i += kBlock) {
+    for (int i = tid; i < (K + 1) * (GP - N); i += BLK) {
         const int k = i / (GP - N), c = N + (i - k * (GP - N));
         sBt[k * GP + c] = 0.0;
         if constexpr (PT) sBP[k * GP + c] = double2{0.0, 0.0};
@@ -1282,7 +1282,7 @@ __device__ bool merged_mstep(const EArgs &a, double *sBt, double2 *sBP, double *
     }
     if constexpr (HIST) {
         double2 *z2 = reinterpret_cast<double2 *>(sBn);
-        for (int i = tid; i < K * GP / 2; i += kBlock) z2[i] = double2{0.0, 0.0};
+        for (int i = tid; i < K * GP / 2; i += BLK) z2[i] = double2{0.0, 0.0};
         if ((K * GP) & 1)
             if (tid == 0) sBn[K * GP - 1] = 0.0;
     }

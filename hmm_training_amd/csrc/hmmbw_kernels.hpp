@@ -24,6 +24,11 @@ struct Kernels {
 template <int N>
 Kernels small_kernels_n(bool lr, bool ldstab);
 
+// Dense-A kernels on the fp64 matrix cores for 5 <= N <= 8 (estep_dmfma.hpp): the small layout,
+// 128-thread workgroups; empty Kernels for other N.
+template <int N>
+Kernels dmfma_kernels_n();
+
 // Wide kernels (16 < N <= 64) for the padded state count NP (32, 48 or 64).
 Kernels wide_kernels(int NP);
 
