@@ -158,6 +158,16 @@ Kernels pick_small_n(int N) {
     }
 }
 
+Kernels pick_lr2_n(int N) {
+    switch (N) {
+        case 5: return lr2_kernels_n<5>();
+        case 6: return lr2_kernels_n<6>();
+        case 7: return lr2_kernels_n<7>();
+        case 8: return lr2_kernels_n<8>();
+        default: return Kernels{};
+    }
+}
+
 Kernels pick_dmfma_n(int N) {
     switch (N) {
         case 5: return dmfma_kernels_n<5>();
@@ -191,6 +201,7 @@ struct hmmbw_ctx {
     int ncopies = 2;              // HMMBW_OPT_STAT_COPIES default: halves the flush atomics per address (measured -3 %)
     bool merge_mstep = true;      // run each M-step in the prologue of the next E-step launch
     int dense_mfma = 0;           // dense A, 5 <= N <= 8, fp64-MFMA kernel (estep_dmfma.hpp): 1 scorer, 2 + E-step
+    int lr_pairs = 0;             // left-to-right, 5 <= N <= 8: two states per lane (estep_lr2.hpp)
     bool armed = false;
     long long e_count = 0;        // E-step launches since the statistics were last cleared
     // an M-step whose statistics are ready but which has not run yet (it runs in the next merged
@@ -403,7 +414,15 @@ int plan_estep(hmmbw_ctx *c, bool fwd_only, const IterState *state, double *copi
         const size_t GP = (size_t)c->G + 1;
         const size_t ntab = ((((size_t)c->K + 1) * GP) + 1) & ~(size_t)1;
         const Kernels km = pick_dmfma_n(c->N);
-        if (!lr && lds_tab && c->dense_mfma >= (fwd_only ? 1 : 2) && allow_dmfma && km.estep) {
+        const Kernels k2 = pick_lr2_n(c->N);
+        if (lr && lds_tab && c->lr_pairs && allow_dmfma && k2.estep) {
+            // left-to-right with two states per lane: 2 waves (two 16-sequence tiles = the small
+            // kernel's 4 waves of sequences) per workgroup, same grid (estep_lr2.hpp)
+            p.fn = fwd_only ? k2.score : k2.estep;
+            p.block = 128;
+            const size_t tabs = 3 * ntab + (fwd_only ? 0 : (size_t)c->K * GP);
+            p.lds = sizeof(double) * (tabs + 2 * (size_t)c->G * 7 + 8);
+        } else if (!lr && lds_tab && c->dense_mfma >= (fwd_only ? 1 : 2) && allow_dmfma && km.estep) {
             // dense A on the fp64 matrix cores: 2 waves (two 16-sequence tiles = the small kernel's 4
             // waves of sequences) per workgroup, same grid (estep_dmfma.hpp)
             p.fn = fwd_only ? km.score : km.estep;
@@ -802,6 +821,10 @@ int hmmbw_set_option(hmmbw_ctx *c, int key, int64_t value) {
         if (int rc = set_device(c)) return rc;
         if (int rc = flush_mstep(c)) return rc;
         c->merge_mstep = value != 0;
+        return HMMBW_OK;
+    }
+    if (key == HMMBW_OPT_LR_PAIRS) {
+        c->lr_pairs = value != 0;
         return HMMBW_OK;
     }
     if (key == HMMBW_OPT_DENSE_MFMA) {

@@ -163,6 +163,10 @@ int hmmbw_score(hmmbw_ctx *ctx, double *out);
  * wave to hide the MFMA and LDS latencies, is 4.6x slower), scorer no faster, hence off by default.
  * Results agree to fp64 rounding either way (tests/test_gpu_dmfma.py). */
 #define HMMBW_OPT_DENSE_MFMA 5
+/* Left-to-right A with 5 <= N <= 8: 1 runs the two-states-per-lane kernel (16 sequences per wave,
+ * estep_lr2.hpp), 0 (default) the one-state-per-lane kernel (8 sequences per wave).  Experimental:
+ * parity-green, but measured 1.8x slower at cfg3 (90 vs 50 us per E-step). */
+#define HMMBW_OPT_LR_PAIRS 6
 int hmmbw_set_option(hmmbw_ctx *ctx, int key, int64_t value);
 
 /* E-step kernel timing with HIP events on the context stream (for bench/roofline).  Returns the
