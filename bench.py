@@ -7,19 +7,36 @@
 
 One step = one full EM iteration (E-step kernel over every sequence of the rank, the RCCL all-reduce
 of the packed statistics when N > 1, the M-step/convergence kernel) on synthetic sequences already
-resident in HBM.  Workload (BASELINE cfg3, per GPU): R=10,000 sequences, T=200, N=8 states, K=256
-symbols, the reference's left-to-right topology (hmm_training.py:307-312, generalised to N=8) and
-uniform random symbols.  Weak scaling: every rank owns 10,000 sequences.
+resident in HBM.  Workloads:
+  N = 1: BASELINE cfg3, R = 10,000 sequences, T = 200, N = 8 states, K = 256 symbols;
+  N > 1: BASELINE cfg4 shards, 12,500 sequences per GPU (N = 8 is exactly cfg4's 100,000), weak
+         scaling (fixed work per GPU);
+  --workload cfg5: 6,250 sequences per GPU, T = 400, N = 64, K = 1024 (the fp64-MFMA wide path).
+The reference's left-to-right topology (hmm_training.py:307-312, generalised to N states) and
+uniform symbols ('U') by default; --symbols H draws them from a ground-truth left-to-right HMM with
+Dirichlet(0.3) emission rows (skewed symbol counts).
+
+--gpus N without a launcher (no WORLD_SIZE in the environment) starts N rank processes itself
+(127.0.0.1 rendezvous) before anything touches the GPU, and exits with their status; under a
+launcher, --gpus must equal WORLD_SIZE.  --dry-run runs the launcher/rendezvous/timing skeleton
+with no GPU work (CPU tests).
 
 Prints ONE JSON line (rank 0) with the driver's fields plus:
   roofline     — achieved = algorithmic bytes per E-step launch (B_u = 24T + 16NT + 8
                  per sequence) / the E-step kernel's mean duration from HIP events on its stream;
                  traffic = measured HBM bytes per launch from the committed rocprofv3 PMC summary
                  (profiles/), or null when none matches this config.  For N > 16 (the fp64-MFMA wide
-                 path, cfg5) the bound is "mfma": achieved = 8 N^2 T flops per sequence / kernel time
-                 against the 78.6 TFLOP/s dense fp64 matrix peak.
-  cpu_baseline — the oracle C restatement (oracle/bw_oracle.c, log domain like the reference) timed on
-                 one host core over a bounded sample of the same workload (rank 0, N=1 only).
+                 path, cfg5) the bound is "mfma": achieved = 8 N^2 T flops per sequence (the survey's
+                 figure) / kernel time against the 78.6 TFLOP/s dense fp64 matrix peak, with the
+                 fraction on the 6 N^2 T flops the kernel actually issues beside it.
+  cpu_baseline — the oracle C restatement (oracle/bw_oracle.c, log domain like the reference) with
+                 OpenMP over utterances on the host cores this process may use, timed on a bounded
+                 sample of the same workload (rank 0, N=1 only), with its ratio to the reference's
+                 own NumPy path measured in the build container.
+  comm         — N > 1: ranks of the RCCL communicator the engine created and the all-reduce
+                 microseconds per iteration (HIP events around ncclAllReduce on the engine stream).
+  synced       — SURVEY §8(d)'s protocol: median of per-iteration times with the 8-byte convergence
+                 read-back after every iteration, and the drop-in train loop's ms per iteration.
 """
 from __future__ import annotations
 
@@ -27,6 +44,8 @@ import argparse
 import glob
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -37,25 +56,56 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 FP64_MFMA_PEAK_TFS = 78.6  # MI355X dense fp64 matrix peak (vendor spec)
+# The reference's own NumPy path at cfg3 shape in the build container (BASELINE.md / SURVEY §6)
+REF_UTT_PER_S_1CORE = 9.39
+REF_UTT_PER_S_8CORES = 79.98
+
+WORKLOADS = {  # name: (sequences per GPU, T, N, K)
+    "cfg3": (10_000, 200, 8, 256),
+    "cfg4": (12_500, 200, 8, 256),
+    "cfg5": (6_250, 400, 64, 1024),
+}
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=50)
     p.add_argument("--warmup", type=int, default=5)
-    p.add_argument("--R", type=int, default=10_000, help="sequences per GPU")
-    p.add_argument("--T", type=int, default=200)
-    p.add_argument("--N", type=int, default=8)
-    p.add_argument("--K", type=int, default=256)
-    p.add_argument("--topology", default="left_to_right", choices=["left_to_right", "dense"])
+    p.add_argument("--workload", default="auto", choices=["auto", *WORKLOADS],
+                   help="auto: cfg3 on one GPU, cfg4 shards (12,500 per GPU) on several")
+    p.add_argument("--R", type=int, default=None, help="sequences per GPU (overrides the workload)")
+    p.add_argument("--T", type=int, default=None)
+    p.add_argument("--N", type=int, default=None)
+    p.add_argument("--K", type=int, default=None)
+    p.add_argument("--topology", default=None, choices=["left_to_right", "dense"],
+                   help="default: left_to_right (dense for cfg5)")
+    p.add_argument("--symbols", default="U", choices=["U", "H"], help="U: uniform; H: skewed, from a ground-truth HMM")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline sample budget")
+    p.add_argument("--cpu-threads", type=int, default=0, help="0: every core this process may use")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--seed", type=int, default=3)
+    p.add_argument("--no-synced", action="store_true", help="skip the synced-protocol and drop-in measurements")
+    p.add_argument("--seed", type=int, default=None)
     p.add_argument("--no-kernel-timing", action="store_true", help="skip the HIP events")
     p.add_argument("--timing-every", type=int, default=5, help="time every k-th E-step launch")
     p.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) on MI355X; gloo only for tests")
-    return p.parse_args()
+    p.add_argument("--dry-run", action="store_true", help="launcher + rendezvous + timing skeleton, no GPU work")
+    return p.parse_args(argv)
+
+
+def resolve_workload(args, world):
+    name = args.workload if args.workload != "auto" else ("cfg3" if world == 1 else "cfg4")
+    R, T, N, K = WORKLOADS[name]
+    custom = any(v is not None for v in (args.R, args.T, args.N, args.K))
+    R = args.R if args.R is not None else R
+    T = args.T if args.T is not None else T
+    N = args.N if args.N is not None else N
+    K = args.K if args.K is not None else K
+    topo = args.topology or ("dense" if name == "cfg5" else "left_to_right")
+    seed = args.seed if args.seed is not None else {"cfg3": 3, "cfg4": 4, "cfg5": 5}[name]
+    if custom:
+        name = f"custom ({name} shape overridden)"
+    return name, R, T, N, K, topo, seed
 
 
 def init_params(N, K, topology, rng):
@@ -66,20 +116,43 @@ def init_params(N, K, topology, rng):
     return pi, A, B
 
 
+def synthetic_symbols(R, T, N, K, kind, seed):
+    """[R*T] int32 symbols.  U: uniform.  H: a ground-truth left-to-right HMM with N
+    states, self-loop 0.9, emission rows ~ Dirichlet(0.3 * 1_K), starting in state 0 — skewed symbol
+    counts and gamma statistics, as on real codebook data."""
+    rng = np.random.default_rng(seed)
+    if kind == "U":
+        return rng.integers(0, K, size=R * T).astype(np.int32)
+    B = rng.dirichlet(np.full(K, 0.3), size=N)
+    cdf = np.cumsum(B, axis=1)
+    cdf[:, -1] = 1.0
+    state = np.zeros(R, dtype=np.int64)
+    out = np.empty((R, T), dtype=np.int32)
+    for t in range(T):
+        if t:
+            state = np.minimum(state + (rng.random(R) < 0.1), N - 1)
+        out[:, t] = _sample_rows(cdf, state, rng.random(R))
+    return np.minimum(out, K - 1).reshape(-1)
+
+
+def _sample_rows(cdf, state, u):
+    res = np.empty(len(state), dtype=np.int32)
+    for s in np.unique(state):
+        m = state == s
+        res[m] = np.searchsorted(cdf[s], u[m], side="right")
+    return res
+
+
 def bytes_per_sequence(T, N):
     return 24 * T + 16 * N * T + 8  # SURVEY §8(d)
 
 
 def flops_per_sequence(T, N):
-    return 8 * N * N * T  # forward + backward + xi, fp64
+    return 8 * N * N * T  # SURVEY §8(d): forward + backward + xi, fp64 (informational figure)
 
 
-def workload_name(R, T, N, K):
-    if (T, N, K) == (200, 8, 256):
-        return "cfg3" if R == 10_000 else ("cfg4" if R == 12_500 else "cfg3-shape")
-    if (T, N, K) == (400, 64, 1024):
-        return "cfg5" if R == 6_250 else "cfg5-shape"
-    return "custom"
+def mfma_flops_issued(T, N):
+    return 6 * N * N * T  # what k_estep_mfma issues: forward 2N^2, backward 2N^2, xi 2N^2 per step
 
 
 def find_traffic(cfg_key):
@@ -96,36 +169,116 @@ def find_traffic(cfg_key):
     return best
 
 
-def cpu_baseline(N, K, T, topology, budget_s, seed):
-    """The oracle (C, log domain, single thread) on a bounded sample of the same workload."""
+def host_threads(requested=0):
+    if requested > 0:
+        return requested
+    env = os.environ.get("OMP_NUM_THREADS", "")
+    if env.isdigit() and int(env) > 0:
+        return int(env)
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(N, K, T, topology, budget_s, seed, symbols="U", threads=0):
+    """The oracle (C, log domain, OpenMP over utterances) on a bounded sample of the same workload."""
     from oracle import oracle as O
     rng = np.random.default_rng(seed + 1000)
     pi, A, B = init_params(N, K, topology, rng)
+    nth = O.set_threads(host_threads(threads))
 
     def run(R):
-        sym = rng.integers(0, K, size=R * T).astype(np.int64)
+        sym = synthetic_symbols(R, T, N, K, symbols, seed + 1000 + R).astype(np.int64)
         off = np.arange(R + 1, dtype=np.int64) * T
         t0 = time.perf_counter()
         O.hmm_training(off, sym, N, K, 0.0, 1, pi, A, B)
         return time.perf_counter() - t0
 
-    probe_R = 8
-    dt = run(probe_R)
-    R = int(max(probe_R, min(200_000, probe_R * budget_s / max(dt, 1e-6))))
-    dt = run(R)
-    return {"value": R / dt, "unit": "utterances/s/iter", "cores": 1, "kind": "port",
-            "sample": f"{R} sequences x 1 EM iteration (T={T}, N={N}, K={K}, {topology}) on the oracle "
-                      f"restatement oracle/bw_oracle.c, 1 thread, {dt:.1f} s"}
+    try:
+        probe_R = 8 * nth
+        dt = run(probe_R)
+        R = int(max(probe_R, min(400_000, probe_R * budget_s / max(dt, 1e-6))))
+        dt = run(R)
+    finally:
+        O.set_threads(1)
+    value = R / dt
+    return {"value": value, "unit": "utterances/s/iter", "cores": nth, "kind": "port",
+            "cpu_model": cpu_model(), "nproc_visible": os.cpu_count(),
+            "sample": f"{R} sequences x 1 EM iteration (T={T}, N={N}, K={K}, {topology}, symbols {symbols}) on the "
+                      f"oracle restatement oracle/bw_oracle.c, OpenMP over utterances on {nth} threads, {dt:.1f} s",
+            "ratio_vs_reference_8cores": value / REF_UTT_PER_S_8CORES,
+            "ratio_per_core_vs_reference": (value / nth) / REF_UTT_PER_S_1CORE,
+            "reference_note": "reference NumPy path (HMM/hmm_training.py) measured in the build container at cfg3 "
+                              "shape: 9.39 utt/s/iter on 1 core, 79.98 on 8 (BASELINE.md); different host"}
 
 
-def main():
-    args = parse()
+def free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch(args, argv):
+    """--gpus N without a launcher: start N rank processes (one per GPU) before any GPU call."""
+    port = free_port()
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env))
+    rc = 0
+    try:
+        pending = list(procs)
+        while pending:
+            for p in list(pending):
+                code = p.poll()
+                if code is None:
+                    continue
+                pending.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code
+                    for q in pending:  # one rank failed: the others would wait forever in a collective
+                        q.terminate()
+            time.sleep(0.05)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    return rc if rc >= 0 else 128 - rc
+
+
+def main(argv=None):
+    argv = list(sys.argv[1:] if argv is None else argv)
+    args = parse(argv)
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        return launch(args, argv)
+    world = int(env_world or 1)
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks", file=sys.stderr)
+        return 2
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    wl, R, T, N, K, topo, seed = resolve_workload(args, world)
+
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dry_run:
+        return dry_run(args, world, rank, wl, R, T, N, K, topo)
+
     device = local_rank % max(torch.cuda.device_count(), 1) if world > 1 else 0
     if world > 1:
         torch.cuda.set_device(device)
@@ -137,23 +290,24 @@ def main():
 
     from hmm_training_amd.engine import BaumWelchEngine
 
-    R, T, N, K = args.R, args.T, args.N, args.K
-    rng = np.random.default_rng(args.seed + 7919 * rank)
-    symbols = rng.integers(0, K, size=R * T).astype(np.int32)
+    symbols = synthetic_symbols(R, T, N, K, args.symbols, seed + 7919 * rank)
     offsets = np.arange(R + 1, dtype=np.int64) * T
-    pi, A, B = init_params(N, K, args.topology, np.random.default_rng(args.seed))
+    pi, A, B = init_params(N, K, topo, np.random.default_rng(seed))
 
-    eng = BaumWelchEngine(N, K, device=device, topology=args.topology, rank=rank, world_size=world)
+    eng = BaumWelchEngine(N, K, device=device, topology=topo, rank=rank, world_size=world)
+    t_up = time.perf_counter()
     eng.set_observations(offsets=offsets, symbols=symbols, n_seq_global=R * world)
     eng.set_params(pi, A, B)
-    assert eng.topology == args.topology
-    total_iters = args.warmup + args.steps
-    eng.reset(0.0, total_iters + 1)  # epsilon 0: no early stop, every timed step is a full iteration
-    stats = eng.make_stats_buffer() if world > 1 else None
+    torch.cuda.synchronize()
+    upload_s = time.perf_counter() - t_up
+    assert eng.topology == topo
+    eng.reset(0.0, 1 << 40)  # epsilon 0: no early stop, every timed step is a full iteration
+    stats = eng.make_stats_buffer() if world > 1 and not eng.native_comm else None
 
     eng.enqueue_iterations(args.warmup, stats)
     torch.cuda.synchronize()
     eng.timing(0 if args.no_kernel_timing else args.timing_every)
+    eng.comm_info(reset=True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -165,27 +319,34 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kern_ms, kern_n = eng.timing(0)
+    comm_ranks, ar_ms, ar_n = eng.comm_info(reset=True)
     st, _ = eng.status()
-    if st.iterations != total_iters:
-        raise RuntimeError(f"expected {total_iters} iterations, engine ran {st.iterations}")
+    if st.iterations != args.warmup + args.steps:
+        raise RuntimeError(f"expected {args.warmup + args.steps} iterations, engine ran {st.iterations}")
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{device}")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+
+    synced = None
+    if not args.no_synced:
+        synced = synced_protocol(eng, stats, world, dist, R)
 
     ms_step = 1000.0 * elapsed / args.steps
     value = R * world * args.steps / elapsed
     kern_s = kern_ms / max(kern_n, 1) / 1000.0
     bu = bytes_per_sequence(T, N)
     wide = N > 16
-    cfg_key = f"R{R}_T{T}_N{N}_K{K}_{args.topology}"
+    cfg_key = f"R{R}_T{T}_N{N}_K{K}_{topo}" + ("_H" if args.symbols == "H" else "")
     traffic = find_traffic(cfg_key)
     if wide:  # fp64 MFMA recursions (estep_mfma.hpp): priced against the dense fp64 matrix peak
         achieved = flops_per_sequence(T, N) * R / kern_s / 1e12 if kern_s > 0 else float("nan")
+        issued = mfma_flops_issued(T, N) * R / kern_s / 1e12 if kern_s > 0 else float("nan")
         roof = {"bound": "mfma", "achieved": achieved, "peak": FP64_MFMA_PEAK_TFS, "unit": "TFLOP/s",
                 "frac": achieved / FP64_MFMA_PEAK_TFS, "traffic": traffic[0] if traffic else None,
                 "kernel": "k_estep_mfma + k_bnum_gather (E-step)", "kernel_ms": kern_s * 1000.0,
                 "flops_per_launch_algorithmic": flops_per_sequence(T, N) * R,
+                "issued_tflops_6N2T": issued, "frac_issued_6N2T": issued / FP64_MFMA_PEAK_TFS,
                 "traffic_source": traffic[1] if traffic else None}
     else:
         achieved = bu * R / kern_s / 1e9 if kern_s > 0 else float("nan")
@@ -194,7 +355,6 @@ def main():
                 "kernel": "k_estep_small (E-step)", "kernel_ms": kern_s * 1000.0,
                 "bytes_per_launch_algorithmic": bu * R,
                 "traffic_source": traffic[1] if traffic else None}
-    wl = workload_name(R, T, N, K)
 
     if rank == 0:
         out = {
@@ -209,25 +369,90 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic (uniform random symbols, seeded); reference-topology random init",
-            "config": {"workload": f"{wl} per GPU: R={R} sequences x T={T}, N={N} states, K={K} symbols, "
-                                   f"{args.topology} A, one EM iteration per step",
-                       "sequences_per_gpu": R, "T": T, "N": N, "K": K, "topology": args.topology,
+            "data": f"synthetic ({'uniform' if args.symbols == 'U' else 'HMM-generated skewed'} symbols, seeded); "
+                    "reference-topology init",
+            "config": {"workload": f"{wl}: R={R} sequences per GPU ({R * world} total) x T={T}, N={N} states, "
+                                   f"K={K} symbols, {topo} A, symbols {args.symbols}, one EM iteration per step",
+                       "sequences_per_gpu": R, "sequences_total": R * world, "T": T, "N": N, "K": K,
+                       "topology": topo, "symbols": args.symbols,
                        "parallelism": f"dp{world}" if world > 1 else "single",
                        "allreduce": ("rccl (engine communicator, engine stream)" if eng.native_comm else
-                                     "torch.distributed") if world > 1 else None},
+                                     f"torch.distributed ({args.dist_backend})") if world > 1 else None},
             "roofline": roof,
+            "comm": {"rccl_comm_ranks": comm_ranks, "allreduce_us_per_iter": 1000.0 * ar_ms / ar_n if ar_n else None,
+                     "allreduce_timed": ar_n, "payload_bytes": 8 * eng.stats_len} if world > 1 else None,
+            "synced": synced,
+            "upload_s": upload_s,
             "loglik_last": st.last_log_likelihood,
         }
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(N, K, T, args.topology, args.cpu_seconds, args.seed)
+            out["cpu_baseline"] = cpu_baseline(N, K, T, topo, args.cpu_seconds, seed, args.symbols, args.cpu_threads)
         else:
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)
     eng.close()
     if world > 1:
         dist.destroy_process_group()
+    return 0
+
+
+def synced_protocol(eng, stats, world, dist, R, iters=10, dropin_iters=20):
+    """median of `iters` EM iterations, each followed by the 8-byte convergence read-back
+    (hmmbw_get_status), plus the drop-in train loop (BaumWelchEngine.train: chunked status syncs)
+    over `dropin_iters` iterations, in ms per iteration."""
+    import torch
+    per = []
+    for _ in range(iters):
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        eng.enqueue_iterations(1, stats)
+        eng.status()  # D2H of the convergence record (synchronises the engine stream)
+        per.append(time.perf_counter() - t0)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    st = eng.train(0.0, dropin_iters)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    med = float(np.median(per))
+    if world > 1:
+        t = torch.tensor([med, dt], dtype=torch.float64, device=f"cuda:{eng.device}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        med, dt = float(t[0]), float(t[1])
+    return {"median_ms_per_iter_with_d2h": 1000.0 * med, "utt_per_s_with_d2h": R * world / med,
+            "dropin_train_ms_per_iter": 1000.0 * dt / max(st.iterations, 1), "dropin_iterations": st.iterations}
+
+
+def dry_run(args, world, rank, wl, R, T, N, K, topo):
+    """No GPU: the process group, barrier and max-over-ranks timing of the real run around a no-op."""
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group("gloo" if args.dist_backend == "gloo" else args.dist_backend)
+        dist.barrier()
+    t0 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    if rank == 0:
+        print(json.dumps({"metric": f"Baum-Welch utterances/sec/iter (T={T},N={N},K={K})", "value": None,
+                          "unit": "utterances/s/iter", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": None, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+                          "dtype": "f64", "data": "dry run (no GPU work)",
+                          "config": {"workload": wl, "sequences_per_gpu": R, "sequences_total": R * world, "T": T,
+                                     "N": N, "K": K, "topology": topo,
+                                     "parallelism": f"dp{world}" if world > 1 else "single"},
+                          "roofline": None, "cpu_baseline": None, "dry_run_barrier_s": elapsed}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -232,6 +232,11 @@ struct hmmbw_ctx {
     // native RCCL communicator (hmmbw_comm_init): the multi-rank hmmbw_iterate all-reduces d_ext
     ncclComm_t comm = nullptr;
     double *d_ext = nullptr;
+    // all-reduce timing (hmmbw_comm_info): event pairs around ncclAllReduce, same schedule as timing
+    long long ar_seq = 0;
+    std::vector<hipEvent_t> ar_free, ar_pending;
+    double ar_ms = 0.0;
+    long long ar_n = 0;
     long long R_global = 0;
     bool has_obs = false;
     int force_safe = 0;
@@ -515,7 +520,34 @@ struct Rccl {
     ncclResult_t (*all_reduce)(const void *, void *, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t,
                                hipStream_t) = nullptr;
     const char *(*error_string)(ncclResult_t) = nullptr;
+    ncclResult_t (*comm_count)(ncclComm_t, int *) = nullptr;  // optional (hmmbw_comm_info)
 };
+
+// HIP event pair from a pool (timing only)
+int take_events(std::vector<hipEvent_t> &pool, hipEvent_t *e0, hipEvent_t *e1) {
+    while (pool.size() < 2) {
+        hipEvent_t x;
+        HIP_TRY(hipEventCreate(&x));
+        pool.push_back(x);
+    }
+    *e1 = pool.back(); pool.pop_back();
+    *e0 = pool.back(); pool.pop_back();
+    return HMMBW_OK;
+}
+
+int drain_pairs(std::vector<hipEvent_t> &pending, std::vector<hipEvent_t> &pool, double *ms_sum, long long *n) {
+    for (size_t i = 0; i + 1 < pending.size(); i += 2) {
+        HIP_TRY(hipEventSynchronize(pending[i + 1]));
+        float ms = 0.f;
+        HIP_TRY(hipEventElapsedTime(&ms, pending[i], pending[i + 1]));
+        *ms_sum += ms;
+        *n += 1;
+        pool.push_back(pending[i]);
+        pool.push_back(pending[i + 1]);
+    }
+    pending.clear();
+    return HMMBW_OK;
+}
 
 int rccl_load(const char *path, Rccl **out) {
     static Rccl r;
@@ -531,6 +563,7 @@ int rccl_load(const char *path, Rccl **out) {
         r.comm_destroy = reinterpret_cast<decltype(r.comm_destroy)>(dlsym(h, "ncclCommDestroy"));
         r.all_reduce = reinterpret_cast<decltype(r.all_reduce)>(dlsym(h, "ncclAllReduce"));
         r.error_string = reinterpret_cast<decltype(r.error_string)>(dlsym(h, "ncclGetErrorString"));
+        r.comm_count = reinterpret_cast<decltype(r.comm_count)>(dlsym(h, "ncclCommCount"));
         if (!r.get_unique_id || !r.comm_init_rank || !r.comm_destroy || !r.all_reduce || !r.error_string)
             return fail(HMMBW_E_UNSUPPORTED, "RCCL library lacks the ncclGetUniqueId / ncclCommInitRank / "
                                              "ncclCommDestroy / ncclAllReduce / ncclGetErrorString symbols");
@@ -626,6 +659,8 @@ int hmmbw_ctx_destroy(hmmbw_ctx *c) {
     free_obs(c);
     for (auto e : c->ev_free) (void)hipEventDestroy(e);
     for (auto e : c->ev_pending) (void)hipEventDestroy(e);
+    for (auto e : c->ar_free) (void)hipEventDestroy(e);
+    for (auto e : c->ar_pending) (void)hipEventDestroy(e);
     delete c;
     return HMMBW_OK;
 }
@@ -928,9 +963,21 @@ int hmmbw_iterate(hmmbw_ctx *c, int64_t n_iter) {
         if (int rc = rccl_load(nullptr, &r)) return rc;
         for (int64_t i = 0; i < n_iter; ++i) {
             if (int rc = hmmbw_estep(c, c->d_ext)) return rc;
+            hipEvent_t e0 = nullptr, e1 = nullptr;
+            if (c->timing && (c->ar_seq++ % c->timing) == 0) {
+                if (int rc = take_events(c->ar_free, &e0, &e1)) return rc;
+                HIP_TRY(hipEventRecord(e0, c->stream));
+            }
             ncclResult_t e = r->all_reduce(c->d_ext, c->d_ext, (size_t)c->stats_len(), ncclFloat64, ncclSum, c->comm,
                                            c->stream);
             if (e != ncclSuccess) return rccl_fail(r, e, "ncclAllReduce");
+            if (e1) {
+                HIP_TRY(hipEventRecord(e1, c->stream));
+                c->ar_pending.push_back(e0);
+                c->ar_pending.push_back(e1);
+                if (c->ar_pending.size() >= 256)
+                    if (int rc = drain_pairs(c->ar_pending, c->ar_free, &c->ar_ms, &c->ar_n)) return rc;
+            }
             if (int rc = hmmbw_mstep(c, c->d_ext, c->R_global)) return rc;
         }
         return HMMBW_OK;
@@ -1201,6 +1248,31 @@ int hmmbw_comm_init(hmmbw_ctx *c, const char *rccl_path, const void *id, int ran
     HIP_TRY(hipMemset(c->d_ext, 0, sizeof(double) * (size_t)c->stats_len()));
     c->comm = comm;
     c->R_global = n_seq_global;
+    return HMMBW_OK;
+}
+
+int hmmbw_comm_info(hmmbw_ctx *c, int *n_ranks, double *total_ms, int64_t *count, int reset) {
+    if (!c) return fail(HMMBW_E_INVALID, "null context");
+    if (int rc = set_device(c)) return rc;
+    int n = 0;
+    if (c->comm) {
+        Rccl *r = nullptr;
+        if (int rc = rccl_load(nullptr, &r)) return rc;
+        n = -1;  // communicator exists but this RCCL has no ncclCommCount
+        if (r->comm_count) {
+            ncclResult_t e = r->comm_count(c->comm, &n);
+            if (e != ncclSuccess) return rccl_fail(r, e, "ncclCommCount");
+        }
+    }
+    if (int rc = drain_pairs(c->ar_pending, c->ar_free, &c->ar_ms, &c->ar_n)) return rc;
+    if (n_ranks) *n_ranks = n;
+    if (total_ms) *total_ms = c->ar_ms;
+    if (count) *count = c->ar_n;
+    if (reset) {
+        c->ar_ms = 0.0;
+        c->ar_n = 0;
+        c->ar_seq = 0;
+    }
     return HMMBW_OK;
 }
 

@@ -280,6 +280,15 @@ class BaumWelchEngine:
         check(self._lib.hmmbw_timing(self._ctx, int(enable), ctypes.byref(ms), ctypes.byref(n)))
         return ms.value, n.value
 
+    def comm_info(self, reset: bool = False) -> Tuple[int, float, int]:
+        """(ranks of the engine's RCCL communicator (0: none), all-reduce ms summed over the timed
+        iterations, number of timed all-reduces) -- hmmbw_comm_info."""
+        n = ctypes.c_int()
+        ms = ctypes.c_double()
+        cnt = ctypes.c_int64()
+        check(self._lib.hmmbw_comm_info(self._ctx, ctypes.byref(n), ctypes.byref(ms), ctypes.byref(cnt), int(reset)))
+        return n.value, ms.value, cnt.value
+
     def close(self) -> None:
         if getattr(self, "_ctx", None):
             self._lib.hmmbw_ctx_destroy(self._ctx)

@@ -211,10 +211,14 @@ def hmm_training(observations: List[np.ndarray], N: int = 4, M: int = 256, epsil
                  max_iterations: int = 100, show_progress=True, word_name: str = None,
                  load_initial_params: bool = True, *, device: Optional[int] = None, topology: str = "auto",
                  group=None) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
-    """Baum-Welch EM for one discrete HMM; returns (A, B, pi) like hmm_training.py:265-541."""
-    pi0, A0, B0 = _initial_params(N, M, word_name, load_initial_params, show_progress)
+    """Baum-Welch EM for one discrete HMM; returns (A, B, pi) like hmm_training.py:265-541.
 
+    Under torch.distributed (world_size > 1) only rank 0 prints the reference's progress lines, so
+    a torchrun of the drop-in shows them once; every rank returns the same parameters."""
     rank, world, group = _dist_context(group)
+    if rank != 0:
+        show_progress = False
+    pi0, A0, B0 = _initial_params(N, M, word_name, load_initial_params, show_progress)
     obs = list(observations)
     if world > 1:
         lo, hi = shard_bounds([len(o) for o in obs], world)[rank]
@@ -239,7 +243,8 @@ def hmm_training(observations: List[np.ndarray], N: int = 4, M: int = 256, epsil
         if st.iterations == 0:
             # the reference's while-loop never ran: :517 reads an unbound local
             raise UnboundLocalError("local variable 'current_log_likelihood_sum' referenced before assignment")
-        _final_lines(st, max_iterations)
+        if rank == 0:
+            _final_lines(st, max_iterations)
         pi, A, B = engine.params(normalise=True)
     finally:
         engine.close()

@@ -1,6 +1,6 @@
 """``train`` / ``test`` entry points of the reference's HMM/main.py (:46-197) on the MI355X engine.
 
-    python -m hmm_training_amd.main train [--max-iterations 100] [--data ../Data]
+    python -m hmm_training_amd.main train [--max-iterations 2] [--data ../Data]
     python -m hmm_training_amd.main test  [--data ../Data]
 
 Same on-disk layout as the reference:
@@ -192,7 +192,8 @@ def _cli(argv=None):
     ap.add_argument("command", choices=["train", "test"])
     ap.add_argument("--data", default="../Data")
     ap.add_argument("--models", default=None, help="model directory (default: DataStorageHMM's)")
-    ap.add_argument("--max-iterations", type=int, default=100)
+    # `python main.py train` runs train_hmm(show_progress=True, max_iterations=2) (HMM/main.py:268)
+    ap.add_argument("--max-iterations", type=int, default=2)
     ap.add_argument("--load-initial-params", action="store_true")
     ap.add_argument("--quiet", action="store_true")
     a = ap.parse_args(argv)

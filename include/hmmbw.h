@@ -125,6 +125,11 @@ int hmmbw_comm_probe(const char *rccl_path); /* HMMBW_OK if the RCCL entry point
 int hmmbw_comm_unique_id(const char *rccl_path, void *id_out);
 int hmmbw_comm_init(hmmbw_ctx *ctx, const char *rccl_path, const void *id, int rank, int world_size,
                     int64_t n_seq_global);
+/* SYNC. The engine communicator as created: *n_ranks = ncclCommCount (0 without a communicator),
+ * plus the HIP-event time of the ncclAllReduce calls hmmbw_iterate enqueued while E-step timing was
+ * on (hmmbw_timing; the same every-k-th schedule), summed in *total_ms over *count calls.  reset=1
+ * clears the accumulated time.  Measurement only (bench.py's all-reduce microseconds per iteration). */
+int hmmbw_comm_info(hmmbw_ctx *ctx, int *n_ranks, double *total_ms, int64_t *count, int reset);
 
 /* SYNC. Status plus the iteration records [first, first+count) (ring of 4096 entries). */
 int hmmbw_get_status(hmmbw_ctx *ctx, hmmbw_status *status, hmmbw_iter_record *records, int64_t first,

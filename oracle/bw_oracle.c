@@ -26,6 +26,9 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
 
 #define NEG_INF (-INFINITY)
 
@@ -100,6 +103,59 @@ static double o_loglik_from_alpha(const double *alpha, int64_t T, int N) {
     return lse_value(&acc);
 }
 
+/* one sequence's terms into the accumulators (the body of :351-410 for utterance r) */
+static void o_accum_seq(const int64_t *obs, int64_t T, int N, int M, const double *lpi, const double *la,
+                        const double *lb, double *alpha, double *beta, lse_t *a_pi, lse_t *a_xi, lse_t *a_gex,
+                        lse_t *a_gall, lse_t *a_b, double *logP_r) {
+    o_forward(obs, T, N, M, lpi, la, lb, alpha);
+    o_backward(obs, T, N, M, la, lb, beta);
+    double lp = o_loglik_from_alpha(alpha, T, N);
+    *logP_r = lp;
+    if (lp == NEG_INF) return;                 /* :391-394, :401-410: gamma and xi all -inf */
+    for (int64_t t = 0; t < T; ++t) {
+        int64_t o = obs[t];
+        for (int i = 0; i < N; ++i) {
+            double g = alpha[(int64_t)i * T + t] + beta[(int64_t)i * T + t] - lp;          /* :392 */
+            if (g == NEG_INF) continue;
+            if (t == 0) lse_add(&a_pi[i], g);                                              /* :420 */
+            if (t < T - 1) lse_add(&a_gex[i], g);                                          /* :436 */
+            lse_add(&a_gall[i], g);                                                        /* :467 */
+            lse_add(&a_b[(int64_t)i * M + o], g);                                          /* :483 */
+        }
+        if (t < T - 1) {
+            int64_t on = obs[t + 1];
+            for (int i = 0; i < N; ++i)
+                for (int j = 0; j < N; ++j) {                                              /* :402-408 */
+                    double x = alpha[(int64_t)i * T + t] + la[i * N + j] + lb[(int64_t)j * M + on] +
+                               beta[(int64_t)j * T + t + 1] - lp;
+                    lse_add(&a_xi[i * N + j], x);
+                }
+        }
+    }
+}
+
+/* merge two online accumulators (the LSE of the union of their term lists) */
+static inline void lse_merge(lse_t *a, const lse_t *b) {
+    if (b->m == NEG_INF) return;
+    if (a->m == NEG_INF) { *a = *b; return; }
+    if (b->m <= a->m) a->s += b->s * exp(b->m - a->m);
+    else { a->s = a->s * exp(a->m - b->m) + b->s; a->m = b->m; }
+}
+
+/* Threads used by oracle_estep_logstats (and so oracle_hmm_training): 1 = the serial restatement
+ * the parity tests use.  bench.py's cpu_baseline leg sets the host's core count (OpenMP over
+ * utterances, per-thread accumulators merged in thread order: same terms, different rounding order). */
+static int g_threads = 1;
+int oracle_set_threads(int n) {
+#ifdef _OPENMP
+    g_threads = n > 0 ? n : 1;
+#else
+    (void)n;
+    g_threads = 1;
+#endif
+    return g_threads;
+}
+
 /*
  * E-step sufficient statistics in the log domain (hmm_training.py:351-410 feeding :415-500):
  *   lpi_num[N]    = LSE_r gamma_0^r(i)                       (:415-424, before "- log R")
@@ -121,48 +177,42 @@ int oracle_estep_logstats(const int64_t *offsets, const int64_t *symbols, int64_
         if (T <= 0) return -2;
         if (T > Tmax) Tmax = T;
     }
-    double *alpha = (double *)malloc(sizeof(double) * (size_t)N * (size_t)(Tmax ? Tmax : 1));
-    double *beta = (double *)malloc(sizeof(double) * (size_t)N * (size_t)(Tmax ? Tmax : 1));
-    lse_t *a_pi = (lse_t *)malloc(sizeof(lse_t) * N), *a_xi = (lse_t *)malloc(sizeof(lse_t) * N * N);
-    lse_t *a_gex = (lse_t *)malloc(sizeof(lse_t) * N), *a_gall = (lse_t *)malloc(sizeof(lse_t) * N);
-    lse_t *a_b = (lse_t *)malloc(sizeof(lse_t) * (size_t)N * M);
-    if (!alpha || !beta || !a_pi || !a_xi || !a_gex || !a_gall || !a_b) {
-        free(alpha); free(beta); free(a_pi); free(a_xi); free(a_gex); free(a_gall); free(a_b);
-        return -1;
-    }
-    for (int i = 0; i < N; ++i) { lse_init(&a_pi[i]); lse_init(&a_gex[i]); lse_init(&a_gall[i]); }
-    for (int i = 0; i < N * N; ++i) lse_init(&a_xi[i]);
-    for (int64_t i = 0; i < (int64_t)N * M; ++i) lse_init(&a_b[i]);
-
-    for (int64_t r = 0; r < R; ++r) {
-        const int64_t *obs = symbols + offsets[r];
-        int64_t T = offsets[r + 1] - offsets[r];
-        o_forward(obs, T, N, M, lpi, la, lb, alpha);
-        o_backward(obs, T, N, M, la, lb, beta);
-        double lp = o_loglik_from_alpha(alpha, T, N);
-        logP[r] = lp;
-        if (lp == NEG_INF) continue;           /* :391-394, :401-410: gamma and xi all -inf */
-        for (int64_t t = 0; t < T; ++t) {
-            int64_t o = obs[t];
-            for (int i = 0; i < N; ++i) {
-                double g = alpha[(int64_t)i * T + t] + beta[(int64_t)i * T + t] - lp;      /* :392 */
-                if (g == NEG_INF) continue;
-                if (t == 0) lse_add(&a_pi[i], g);                                          /* :420 */
-                if (t < T - 1) lse_add(&a_gex[i], g);                                      /* :436 */
-                lse_add(&a_gall[i], g);                                                    /* :467 */
-                lse_add(&a_b[(int64_t)i * M + o], g);                                      /* :483 */
-            }
-            if (t < T - 1) {
-                int64_t on = obs[t + 1];
-                for (int i = 0; i < N; ++i)
-                    for (int j = 0; j < N; ++j) {                                          /* :402-408 */
-                        double x = alpha[(int64_t)i * T + t] + la[i * N + j] + lb[(int64_t)j * M + on] +
-                                   beta[(int64_t)j * T + t + 1] - lp;
-                        lse_add(&a_xi[i * N + j], x);
-                    }
-            }
+    int nth = g_threads;
+    if (R < nth) nth = R > 0 ? (int)R : 1;
+    /* per thread: N + N*N + N + N + N*M accumulators */
+    const size_t nacc = (size_t)N * (3 + N) + (size_t)N * M;
+    lse_t *acc = (lse_t *)malloc(sizeof(lse_t) * nacc * nth);
+    if (!acc) return -1;
+    for (size_t i = 0; i < nacc * nth; ++i) lse_init(&acc[i]);
+    int fail = 0;
+#ifdef _OPENMP
+#pragma omp parallel num_threads(nth) reduction(| : fail)
+#endif
+    {
+        int tid = 0;
+#ifdef _OPENMP
+        tid = omp_get_thread_num();
+#endif
+        lse_t *a_pi = acc + nacc * tid, *a_xi = a_pi + N, *a_gex = a_xi + N * N, *a_gall = a_gex + N;
+        lse_t *a_b = a_gall + N;
+        double *alpha = (double *)malloc(sizeof(double) * (size_t)N * (size_t)(Tmax ? Tmax : 1));
+        double *beta = (double *)malloc(sizeof(double) * (size_t)N * (size_t)(Tmax ? Tmax : 1));
+        if (!alpha || !beta) {
+            fail = 1;
+        } else {
+            /* contiguous blocks of utterances per thread (static schedule): a fixed merge order */
+            int64_t lo = R * tid / nth, hi = R * (tid + 1) / nth;
+            for (int64_t r = lo; r < hi; ++r)
+                o_accum_seq(symbols + offsets[r], offsets[r + 1] - offsets[r], N, M, lpi, la, lb, alpha, beta,
+                            a_pi, a_xi, a_gex, a_gall, a_b, &logP[r]);
         }
+        free(alpha);
+        free(beta);
     }
+    if (fail) { free(acc); return -1; }
+    for (int th = 1; th < nth; ++th)
+        for (size_t i = 0; i < nacc; ++i) lse_merge(&acc[i], &acc[nacc * th + i]);
+    const lse_t *a_pi = acc, *a_xi = a_pi + N, *a_gex = a_xi + N * N, *a_gall = a_gex + N, *a_b = a_gall + N;
     for (int i = 0; i < N; ++i) {
         lpi_num[i] = lse_value(&a_pi[i]);
         lgden_ex[i] = lse_value(&a_gex[i]);
@@ -170,7 +220,7 @@ int oracle_estep_logstats(const int64_t *offsets, const int64_t *symbols, int64_
     }
     for (int i = 0; i < N * N; ++i) lxi[i] = lse_value(&a_xi[i]);
     for (int64_t i = 0; i < (int64_t)N * M; ++i) lbnum[i] = lse_value(&a_b[i]);
-    free(alpha); free(beta); free(a_pi); free(a_xi); free(a_gex); free(a_gall); free(a_b);
+    free(acc);
     return 0;
 }
 

@@ -45,8 +45,16 @@ def load():
         lib.oracle_vq.argtypes = [_dp, ctypes.c_int64, _dp, ctypes.c_int64, ctypes.c_int, _ip, _dp]
         lib.oracle_lse.restype = ctypes.c_double
         lib.oracle_lse.argtypes = [_dp, ctypes.c_int64]
+        lib.oracle_set_threads.restype = ctypes.c_int
+        lib.oracle_set_threads.argtypes = [ctypes.c_int]
         _lib = lib
     return _lib
+
+
+def set_threads(n: int) -> int:
+    """OpenMP threads of the E-step (over utterances); 1 = the serial restatement the parity tests
+    use.  Returns the count in effect.  Only bench.py's cpu_baseline leg raises it."""
+    return int(load().oracle_set_threads(int(n)))
 
 
 def to_csr(observations: Sequence[np.ndarray]) -> Tuple[np.ndarray, np.ndarray]:

@@ -22,8 +22,40 @@ def _json_line(out):
 def test_cpu_baseline_sample_is_bounded():
     sys.path.insert(0, ROOT)
     import bench
-    cb = bench.cpu_baseline(8, 256, 200, "left_to_right", 0.5, 3)
-    assert cb["kind"] == "port" and cb["cores"] == 1 and cb["value"] > 0 and cb["unit"] == "utterances/s/iter"
+    cb = bench.cpu_baseline(8, 256, 200, "left_to_right", 0.5, 3, threads=2)
+    assert cb["kind"] == "port" and cb["cores"] == 2 and cb["value"] > 0 and cb["unit"] == "utterances/s/iter"
+    assert cb["ratio_vs_reference_8cores"] > 0 and cb["cpu_model"]
+
+
+def test_bench_spawns_ranks_without_launcher():
+    """`bench.py --gpus 2` with no torchrun: bench.py starts both ranks itself (127.0.0.1 rendezvous,
+    nothing touching a GPU before the spawn) and rank 0 reports n_gpus 2 (dry run: no GPU here)."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--dist-backend", "gloo", "--dry-run"],
+                       cwd=ROOT, capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _json_line(r.stdout)
+    assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "dp2"
+    assert d["config"]["sequences_per_gpu"] == 12_500 and d["config"]["workload"] == "cfg4"
+
+
+def test_bench_rejects_gpus_world_mismatch():
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "1", "--dry-run"], cwd=ROOT, capture_output=True,
+                       text=True, timeout=300, env=env)
+    assert r.returncode != 0 and "WORLD_SIZE" in r.stderr
+
+
+def test_skewed_symbols_are_skewed_and_seeded():
+    sys.path.insert(0, ROOT)
+    import numpy as np
+    import bench
+    u = bench.synthetic_symbols(500, 200, 8, 256, "U", 3)
+    h = bench.synthetic_symbols(500, 200, 8, 256, "H", 3)
+    assert h.dtype == np.int32 and h.min() >= 0 and h.max() < 256
+    np.testing.assert_array_equal(h, bench.synthetic_symbols(500, 200, 8, 256, "H", 3))
+    cu, ch = np.bincount(u, minlength=256), np.bincount(h, minlength=256)
+    assert ch.max() > 4 * cu.max()  # hot symbols
 
 
 @pytest.mark.gpu
@@ -55,3 +87,25 @@ def test_bench_two_ranks_one_gpu_gloo():
     d = _json_line(r.stdout)
     assert d["n_gpus"] == 2 and d["scaling"] == "weak" and d["cpu_baseline"] is None
     assert d["config"]["parallelism"] == "dp2"
+
+
+@pytest.mark.gpu
+def test_bench_self_spawned_two_ranks_one_gpu_gloo():
+    """`bench.py --gpus 2` without a launcher on the one-GPU box (both ranks on cuda:0, gloo carrying
+    the all-reduce): the real E-step/all-reduce/M-step loop, n_gpus 2 in the line."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--steps", "5", "--warmup", "1", "--R", "2000",
+                        "--dist-backend", "gloo"], cwd=ROOT, capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _json_line(r.stdout)
+    assert d["n_gpus"] == 2 and d["value"] > 0 and d["config"]["sequences_total"] == 4000
+    assert d["comm"]["rccl_comm_ranks"] == 0 and d["synced"]["dropin_iterations"] == 20
+
+
+@pytest.mark.gpu
+def test_bench_skewed_symbols_line():
+    r = subprocess.run([sys.executable, "bench.py", "--steps", "5", "--warmup", "1", "--symbols", "H",
+                        "--no-cpu-baseline"], cwd=ROOT, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _json_line(r.stdout)
+    assert d["config"]["symbols"] == "H" and d["value"] > 0

@@ -415,3 +415,5 @@ def test_dropin_two_processes_gloo(case, tmp_path):
         assert_params(pi, d["out_pi"], f"pi rank {rank}")
         if rank == 0:
             assert lines == list(d["stdout"])
+        else:
+            assert lines == [], "only rank 0 prints the reference's progress lines"

@@ -96,3 +96,39 @@ def test_oracle_estep_stats_consistency(oracle):
     np.testing.assert_allclose(np.exp(s.log_xi).sum(1), np.exp(s.log_gden_excl), rtol=1e-12)
     np.testing.assert_allclose(np.exp(s.log_bnum).sum(1), np.exp(s.log_gden_all), rtol=1e-12)
     np.testing.assert_allclose(np.exp(s.log_pi_num).sum(), len(d["offsets"]) - 1, rtol=1e-12)
+
+
+def test_oracle_under_asan():
+    """The C restatement under AddressSanitizer + UBSan (oracle/asan_main.c drives every entry point,
+    edge cases included: T=1, T=0 error return, impossible sequences, empty B columns, N=1, more
+    OpenMP threads than sequences, VQ)."""
+    import subprocess
+    from oracle.build_oracle import build_asan
+    exe = build_asan()
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300,
+                       env={**__import__("os").environ, "ASAN_OPTIONS": "detect_leaks=1:abort_on_error=1"})
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "asan ok" in r.stdout
+
+
+def test_oracle_threads_match_serial(oracle):
+    """The OpenMP E-step (bench.py's CPU baseline) sums the same terms as the serial restatement:
+    equal to rounding (per-thread accumulators merged in thread order)."""
+    rng = np.random.default_rng(11)
+    N, K, R = 8, 256, 61
+    lengths = rng.integers(1, 150, size=R)
+    off = np.concatenate([[0], np.cumsum(lengths)]).astype(np.int64)
+    sym = rng.integers(0, K, size=int(off[-1])).astype(np.int64)
+    pi = rng.dirichlet(np.ones(N))
+    A = rng.dirichlet(np.ones(N), size=N)
+    B = rng.dirichlet(np.ones(K), size=N)
+    one = oracle.hmm_training(off, sym, N, K, 1e-6, 3, pi, A, B)
+    try:
+        assert oracle.set_threads(5) == 5
+        many = oracle.hmm_training(off, sym, N, K, 1e-6, 3, pi, A, B)
+    finally:
+        oracle.set_threads(1)
+    np.testing.assert_allclose(many.logP, one.logP, rtol=1e-13)  # params differ by M-step rounding only
+    np.testing.assert_allclose(many.trace_L, one.trace_L, rtol=1e-13)
+    for a, b in ((many.A, one.A), (many.B, one.B), (many.pi, one.pi)):
+        np.testing.assert_allclose(a, b, rtol=1e-11, atol=1e-300)
