@@ -41,8 +41,6 @@ OPT_SAFE_SCALING = 1
 OPT_ABLATE = 2
 OPT_STAT_COPIES = 3
 OPT_MERGE_MSTEP = 4
-OPT_DENSE_MFMA = 5
-OPT_LR_PAIRS = 6
 
 
 class HMMBWError(RuntimeError):

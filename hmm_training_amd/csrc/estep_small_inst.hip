@@ -1,7 +1,5 @@
 // estep_small_inst.hip — instantiates the small-N E-step / scorer kernels for N = HMMBW_INST_N
 // (the build compiles this file once per N = 1..16, in parallel).
-#include "estep_dmfma.hpp"
-#include "estep_lr2.hpp"
 #include "hmmbw_kernels.hpp"
 
 #ifndef HMMBW_INST_N
@@ -24,20 +22,6 @@ Kernels small_kernels_n<HMMBW_INST_N>(bool lr, bool ldstab) {
         return Kernels{k_estep_small<N, G, false, true, false>, k_estep_small<N, G, false, true, true>,
                        k_estep_small_group<N, G, false, true, false>, k_estep_small_group<N, G, false, true, true>};
     return Kernels{k_estep_small<N, G, false, false, false>, k_estep_small<N, G, false, false, true>};
-}
-
-template <>
-Kernels dmfma_kernels_n<HMMBW_INST_N>() {
-    constexpr int N = HMMBW_INST_N;
-    if constexpr (N >= 5 && N <= 8) return Kernels{k_estep_dmfma<N, false>, k_estep_dmfma<N, true>};
-    else return Kernels{};
-}
-
-template <>
-Kernels lr2_kernels_n<HMMBW_INST_N>() {
-    constexpr int N = HMMBW_INST_N;
-    if constexpr (N >= 5 && N <= 8) return Kernels{k_estep_lr2<N, false>, k_estep_lr2<N, true>};
-    else return Kernels{};
 }
 
 }  // namespace hmmbw

@@ -158,26 +158,6 @@ Kernels pick_small_n(int N) {
     }
 }
 
-Kernels pick_lr2_n(int N) {
-    switch (N) {
-        case 5: return lr2_kernels_n<5>();
-        case 6: return lr2_kernels_n<6>();
-        case 7: return lr2_kernels_n<7>();
-        case 8: return lr2_kernels_n<8>();
-        default: return Kernels{};
-    }
-}
-
-Kernels pick_dmfma_n(int N) {
-    switch (N) {
-        case 5: return dmfma_kernels_n<5>();
-        case 6: return dmfma_kernels_n<6>();
-        case 7: return dmfma_kernels_n<7>();
-        case 8: return dmfma_kernels_n<8>();
-        default: return Kernels{};
-    }
-}
-
 }  // namespace hmmbw
 
 using namespace hmmbw;
@@ -200,8 +180,6 @@ struct hmmbw_ctx {
     double *d_copies = nullptr;   // [3][ncopies][copy_len] E-step accumulators (iteration e uses e % 3)
     int ncopies = 2;              // HMMBW_OPT_STAT_COPIES default: halves the flush atomics per address (measured -3 %)
     bool merge_mstep = true;      // run each M-step in the prologue of the next E-step launch
-    int dense_mfma = 0;           // dense A, 5 <= N <= 8, fp64-MFMA kernel (estep_dmfma.hpp): 1 scorer, 2 + E-step
-    int lr_pairs = 0;             // left-to-right, 5 <= N <= 8: two states per lane (estep_lr2.hpp)
     bool armed = false;
     long long e_count = 0;        // E-step launches since the statistics were last cleared
     // an M-step whose statistics are ready but which has not run yet (it runs in the next merged
@@ -256,8 +234,11 @@ struct hmmbw_ctx {
     long long stats_len() const { return off_ll() + 2LL * world; }
     long long copy_len() const { return off_ll(); }
     // emission table + B-numerator histogram in LDS ([K][G+1] fp64 each) when they fit 48 KiB
-    bool lds_tables() const { return !wide && (size_t)(2 * K + 1) * (G + 1) * sizeof(double) <= 48 * 1024; }
-    // the merged M-step needs the LDS tables and the statistics in one register batch per thread
+    // emission P/H tables in LDS (two [K+1][G+1] tables of 16-B entries kHistOff bytes apart, see
+    // hmmbw_device.hpp) when the first fits below kHistOff (the row offsets then fit the uint16 packs)
+    bool lds_tables() const { return !wide && lds_tables_fit(K, G + 1); }
+    // LDS doubles of the small kernels' tables
+    size_t lds_table_doubles() const { return lds_tables() ? lds_table_bytes(K, G + 1) / sizeof(double) : 0; }
     bool can_merge() const { return merge_mstep && lds_tables() && copy_len() <= kMergedMaxStats && nwaves > 0; }
     IterState *state() const { return d_state + scur; }
     double *copies(long long e) const { return d_copies + (e % 3) * (long long)ncopies * copy_len(); }
@@ -392,7 +373,7 @@ struct Plan {
 // E-step launch e accumulates into copies and llpart; it clears `zero` (zero_len doubles) and, when
 // `merge` is set, first runs the pending M-step in its prologue (which consumes c->pend).
 int plan_estep(hmmbw_ctx *c, bool fwd_only, const IterState *state, double *copies, double *llpart, double *zero,
-               long long zero_len, bool merge, Plan *P, bool allow_dmfma = true) {
+               long long zero_len, bool merge, Plan *P) {
     Plan &p = *P;
     p = Plan{};
     EArgs &a = p.a;
@@ -416,32 +397,14 @@ int plan_estep(hmmbw_ctx *c, bool fwd_only, const IterState *state, double *copi
     } else {
         const bool lr = c->topo == HMMBW_TOPOLOGY_LEFT_TO_RIGHT;
         const bool lds_tab = c->lds_tables();
-        const size_t GP = (size_t)c->G + 1;
-        const size_t ntab = ((((size_t)c->K + 1) * GP) + 1) & ~(size_t)1;
-        const Kernels km = pick_dmfma_n(c->N);
-        const Kernels k2 = pick_lr2_n(c->N);
-        if (lr && lds_tab && c->lr_pairs && allow_dmfma && k2.estep) {
-            // left-to-right with two states per lane: 2 waves (two 16-sequence tiles = the small
-            // kernel's 4 waves of sequences) per workgroup, same grid (estep_lr2.hpp)
-            p.fn = fwd_only ? k2.score : k2.estep;
-            p.block = 128;
-            const size_t tabs = 3 * ntab + (fwd_only ? 0 : (size_t)c->K * GP);
-            p.lds = sizeof(double) * (tabs + 2 * (size_t)c->G * 7 + 8);
-        } else if (!lr && lds_tab && c->dense_mfma >= (fwd_only ? 1 : 2) && allow_dmfma && km.estep) {
-            // dense A on the fp64 matrix cores: 2 waves (two 16-sequence tiles = the small kernel's 4
-            // waves of sequences) per workgroup, same grid (estep_dmfma.hpp)
-            p.fn = fwd_only ? km.score : km.estep;
-            p.block = 128;
-            const size_t tabs = ntab + (fwd_only ? 0 : (size_t)c->K * GP + 2 * 2 * 16 * 17);
-            p.lds = sizeof(double) * (tabs + 2 * (size_t)c->G * 3 + 8);
-        } else {
+        {
             Kernels ks = lr ? (lds_tab ? pick_small_n<true, true>(c->N) : pick_small_n<true, false>(c->N))
                             : (lds_tab ? pick_small_n<false, true>(c->N) : pick_small_n<false, false>(c->N));
             p.fn = fwd_only ? ks.score : ks.estep;
             p.gfn = fwd_only ? ks.group_score : ks.group_estep;
             if (!p.fn) return fail(HMMBW_E_UNSUPPORTED, "no kernel for N");
             const int NV = (lr ? 2 : c->N) + 3;
-            const size_t tabs = lds_tab ? ntab * (lr ? 3 : 1) + (fwd_only ? 0 : (size_t)c->K * GP) : 0;
+            const size_t tabs = c->lds_table_doubles();
             p.lds = sizeof(double) * (tabs + (size_t)wpb * c->G * NV + 8);
         }
     }
@@ -757,10 +720,10 @@ int hmmbw_set_observations(hmmbw_ctx *c, const int64_t *offsets, const int32_t *
             sptot += nch * U;
         }
     }
-    // packs hold LDS byte offsets of the emission rows when the tables live in LDS (< 48 KiB, so
-    // they fit uint16), symbol ids otherwise
+    // packs hold LDS byte offsets of the emission record rows when the tables live in LDS (< 64 KiB,
+    // so they fit uint16), symbol ids otherwise
     const bool lds_off = c->lds_tables();
-    const long long row_bytes = (long long)(c->G + 1) * 2 * (long long)sizeof(double);  // 16-B entries
+    const long long row_bytes = (long long)(c->G + 1) * 16;  // 16-B table entries
     std::vector<uint16_t> hsym((size_t)std::max(symtot, 1LL), 0);
     for (long long w = 0; w < nwaves; ++w)
         for (int u = 0; u < U; ++u) {
@@ -856,15 +819,6 @@ int hmmbw_set_option(hmmbw_ctx *c, int key, int64_t value) {
         if (int rc = set_device(c)) return rc;
         if (int rc = flush_mstep(c)) return rc;
         c->merge_mstep = value != 0;
-        return HMMBW_OK;
-    }
-    if (key == HMMBW_OPT_LR_PAIRS) {
-        c->lr_pairs = value != 0;
-        return HMMBW_OK;
-    }
-    if (key == HMMBW_OPT_DENSE_MFMA) {
-        if (value < 0 || value > 2) return fail(HMMBW_E_INVALID, "dense MFMA mode must be 0, 1 or 2");
-        c->dense_mfma = (int)value;
         return HMMBW_OK;
     }
     if (key == HMMBW_OPT_ABLATE) {  // diagnostics: results are wrong while set
@@ -1352,7 +1306,7 @@ int hmmbw_group_iterate(hmmbw_group *g, int64_t n_iter) {
                     const long long nz = (long long)c->ncopies * c->copy_len();
                     Plan &p = plans[(size_t)l * n + i];
                     if (int rc = plan_estep(c, false, c->state(), c->copies(e), c->llpart(e), c->copies(e + 1), nz,
-                                            true, &p, false))
+                                            true, &p))
                         return rc;
                     if (!p.gfn || p.gfn != plans[0].gfn || p.block != kBlock)
                         return fail(HMMBW_E_UNSUPPORTED, "group members need the same grouped kernel");
@@ -1389,7 +1343,7 @@ int hmmbw_group_score(hmmbw_group *g, double *out) {
     for (int i = 0; i < n; ++i) {
         hmmbw_ctx *c = g->m[(size_t)i];
         if (int rc = flush_mstep(c)) return rc;
-        if (int rc = plan_estep(c, true, nullptr, nullptr, nullptr, nullptr, 0, false, &plans[(size_t)i], false))
+        if (int rc = plan_estep(c, true, nullptr, nullptr, nullptr, nullptr, 0, false, &plans[(size_t)i]))
             return rc;
         if (!plans[(size_t)i].gfn || plans[(size_t)i].gfn != plans[0].gfn)
             return fail(HMMBW_E_UNSUPPORTED, "group members need the same grouped kernel");

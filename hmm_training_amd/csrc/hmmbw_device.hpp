@@ -47,7 +47,10 @@ static __device__ unsigned long long g_chunk[4096][2][64];
 
 constexpr int kWave = 64;
 constexpr int kChunk = 8;  // time steps per packed symbol load (8 x uint16 = 16 B)
-constexpr int kScale = 4;  // lagged mode: the forward rescales every kScale steps
+#ifndef HMMBW_KSCALE
+#define HMMBW_KSCALE 8
+#endif
+constexpr int kScale = HMMBW_KSCALE;  // lagged mode: the forward rescales every kScale steps
 constexpr int kHist = 4096;
 constexpr int kBlock = 256;  // threads per E-step workgroup (4 waves)
 
@@ -264,8 +267,20 @@ __device__ void block_ll_partial(double lp, bool valid, double *sh, double *out)
 //   gamma_t(i) = z_t(i) beta_hat_t(i),  xi_t(i,j) = a_ij z_t(i) v_j  (accumulated as S_ij = xi/a_ij).
 // gamma is scattered into the per-workgroup LDS histogram B_num[o_t][j] (ds_add_f64).
 // ---------------------------------------------------------------------------------------------
-template <int N, int G, int GP, bool HIST, bool PT, int BLK = kBlock>
-__device__ bool merged_mstep(const EArgs &a, double *sBt, double2 *sBP, double *sBn, double *sPA, long long bid);
+// LDS emission tables of the small kernels: two [(K + 1) x GP] tables of 16-byte entries, row K zero
+// (the padding symbol of ragged waves), the second kHistOff bytes after the first:
+//   P-table {x, y}: left-to-right x = a_jj b_j(o), y = a_{j-1,j} b_j(o) (the two products of the
+//                   forward step); dense x = b_j(o), y = 0;
+//   H-table {h, b}: h = the workgroup's B-numerator histogram (hmm_training.py:474-485), b = b_j(o).
+// The symbol packs hold the byte offset of the symbol's row, o * GP * 16, so ONE lane address per step
+// serves the emission read (ds_read_b128, offset 0) and the histogram add (ds_add_f64, offset
+// kHistOff): the constant distance is the instructions' immediate offset.
+constexpr int kHistOff = 40960;
+__host__ __device__ constexpr bool lds_tables_fit(int K, int GP) { return (size_t)(K + 1) * GP * 16 <= (size_t)kHistOff; }
+__host__ __device__ constexpr size_t lds_table_bytes(int K, int GP) { return (size_t)kHistOff + (size_t)(K + 1) * GP * 16; }
+
+template <int N, int G, int GP, bool PT, int BLK = kBlock>
+__device__ bool merged_mstep(const EArgs &a, double *sP, double *sH, double *sPA, long long bid);
 
 // Body of the small-N E-step / scorer for workgroup `bid` of the `nblk` workgroups that cover one
 // model's sequences: the whole grid of k_estep_small, or one model's slice of a grouped launch
@@ -287,23 +302,22 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
             a.zero[i] = 0.0;
     const int j = lane & (G - 1), u = lane / G;
     const int K = a.K;
-    const size_t ntab = LDSTAB ? (((size_t)K + 1) * GP + 1) & ~(size_t)1 : 0;  // even: 16-B alignment
-    double *sBt = smem;                                               // [K+1][GP] b_j(o)
-    double2 *sBP = reinterpret_cast<double2 *>(smem + ntab);          // PT: [K+1][GP] products
-    double *sBn = smem + ntab + (PT ? 2 * ntab : 0);                  // [K][GP] B numerator histogram
-    double *sRed = sBn + ((LDSTAB && !FWD_ONLY) ? (size_t)K * GP : 0); // [waves][G][NV] + ll scratch
+    double *sP = smem;                   // LDSTAB: P-table [K+1][GP] {x, y} (see kHistOff)
+    double *sH = smem + kHistOff / 8;    // LDSTAB: H-table [K+1][GP] {h, b}
+    double *sRed = smem + (LDSTAB ? lds_table_bytes(K, GP) / 8 : 0);  // [waves][G][NV] + ll scratch
     bool merged = false;
     if constexpr (LDSTAB && !FWD_ONLY) merged = a.merged != 0;
     if (merged) {
         // the previous iteration's M-step, computed redundantly by every workgroup straight into
         // its LDS tables (no separate M-step kernel, no parameter round trip through HBM)
         if constexpr (LDSTAB && !FWD_ONLY)
-            if (!merged_mstep<N, G, GP, true, PT>(a, sBt, sBP, sBn, sPA, bid)) return;  // done or stopped (:346)
+            if (!merged_mstep<N, G, GP, PT>(a, sP, sH, sPA, bid)) return;  // done or stopped (:346)
     } else {
         if (a.state != nullptr && a.state->done) return;  // converged: device-side no-op
         if (tid < G) sPA[tid] = tid < N ? a.pi[tid] : 0.0;
         if (tid < N * N) sPA[G + tid] = a.A[tid];
         if constexpr (LDSTAB) {
+            if constexpr (PT) __syncthreads();  // the records fold a_jj, a_{j-1,j} in
             // 16 independent loads in flight per thread before the first LDS store
             constexpr int TB = 16;
             const int nt = (K + 1) * GP;
@@ -321,26 +335,21 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
                 for (int q = 0; q < TB; ++q) {
                     const int i = i0 + q * kBlock + tid;
                     if (i < nt) {
-                        sBt[i] = x[q];
-                        if constexpr (!FWD_ONLY)
-                            if (i < K * GP) sBn[i] = 0.0;
+                        if constexpr (PT) {
+                            const int c = i % GP;
+                            const double ad = c < N ? sPA[G + c * N + c] : 0.0;
+                            const double ai = (c >= 1 && c < N) ? sPA[G + (c - 1) * N + c] : 0.0;
+                            reinterpret_cast<double2 *>(sP)[i] = double2{ad * x[q], ai * x[q]};
+                        } else {
+                            reinterpret_cast<double2 *>(sP)[i] = double2{x[q], 0.0};
+                        }
+                        reinterpret_cast<double2 *>(sH)[i] = double2{0.0, x[q]};
                     }
                 }
             }
         }
         __syncthreads();
-        if constexpr (PT) {
-            for (int i = tid; i < (K + 1) * GP; i += kBlock) {
-                const int c = i % GP;
-                const double b = sBt[i];
-                const double ad = c < N ? sPA[G + c * N + c] : 0.0;
-                const double ai = (c >= 1 && c < N) ? sPA[G + (c - 1) * N + c] : 0.0;
-                sBP[i] = double2{ad * b, ai * b};
-            }
-            __syncthreads();
-        }
     }
-    const double *Btab = LDSTAB ? sBt : a.Bt;
     PHASE(1);
 
     const long long wave = bid * (blockDim.x >> 6) + wv;
@@ -384,19 +393,18 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
         auto loadpack = [&](int c) -> uint4 {
             return *reinterpret_cast<const uint4 *>(symw + (long long)c * U * kChunk);
         };
-        // Emission-table element of this lane for packed entry k.  With LDS tables the packs hold the
-        // byte offset of the symbol's row in the 16-byte product table (o * GP * 16, precomputed on
-        // the host; half of it in the 8-byte tables), else the symbol.
-        const char *tabj = reinterpret_cast<const char *>(Btab + j);
-        auto brow = [&](const uint4 &p, int k) -> const double * {
-            if constexpr (LDSTAB) return reinterpret_cast<const double *>(tabj + (sym_of(p, k) >> 1));
-            else return reinterpret_cast<const double *>(tabj) + (size_t)sym_of(p, k) * GP;
+        // This lane's P-table entry for packed entry k.  With LDS tables the packs hold the byte
+        // offset of the symbol's row (o * GP * 16, precomputed on the host), else the symbol.
+        char *pj = reinterpret_cast<char *>(sP) + j * 16;
+        auto pent = [&](const uint4 &p, int k) -> char * { return pj + sym_of(p, k); };
+        auto brow = [&](const uint4 &p, int k) -> const double * {  // b_j(o) (and b_{j+1}(o) after it, global)
+            if constexpr (LDSTAB) return reinterpret_cast<const double *>(pent(p, k));
+            else return a.Bt + j + (size_t)sym_of(p, k) * G;
         };
         // the emission operand of one step: the product pair (PT) or b_j(o)
         using Em = typename std::conditional<PT, double2, double>::type;
-        const char *tabPj = reinterpret_cast<const char *>(sBP + j);
         auto ld_em = [&](const uint4 &p, int k) -> Em {
-            if constexpr (PT) return *reinterpret_cast<const double2 *>(tabPj + sym_of(p, k));
+            if constexpr (PT) return *reinterpret_cast<const double2 *>(pent(p, k));
             else return *brow(p, k);
         };
         // One forward step (hmm_training.py:122-160 without the 2^-s rescale, which the caller
@@ -447,7 +455,9 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
             uint4 Q[4];
 #pragma unroll
             for (int i = 0; i < 4; ++i) Q[i] = loadpack(i < nch ? i : nch - 1);
-            const double b00 = *brow(Q[0], 0);  // b_j(o_0) for pi_j b_j(o_0) (:357-360)
+            double b00;  // b_j(o_0) for pi_j b_j(o_0) (:357-360)
+            if constexpr (PT) b00 = *reinterpret_cast<const double *>(pent(Q[0], 0) + kHistOff + 8);  // H.b
+            else b00 = *brow(Q[0], 0);
             Em E[2][kChunk];
 #pragma unroll
             for (int k = 0; k < kChunk; ++k) E[0][k] = ld_em(Q[0], k);
@@ -585,12 +595,21 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
                             if constexpr (LR) fus[k] = scaled ? pow2_scale(bu[k], sk[k]) : bu[k];
                         }
                     }
-                    // recompute z_{8c .. 8c+7} from the checkpoint (identical ops to the forward)
+                    // recompute z_{8c .. 8c+7} from the checkpoint (identical ops to the forward); PT keeps
+                    // the diagonal products ux[k] = a_jj b_j(o_{8c+k}) z_{8c+k-1}(j): xi_t(j,j) = ux[t+1] v_j
                     double zr[kChunk];
+                    double ux[kChunk];
                     zr[0] = cur.ck;
+                    ux[0] = 0.0;
 #pragma unroll
                     for (int k = 1; k < kChunk; ++k) {
-                        const double x = step(zr[k - 1], bv[k]);
+                        double x;
+                        if constexpr (PT) {
+                            ux[k] = bv[k].x * zr[k - 1];
+                            x = fma(bv[k].y, dpp<0x111>(zr[k - 1]), ux[k]);  // = step(zr[k - 1], bv[k])
+                        } else {
+                            x = step(zr[k - 1], bv[k]);
+                        }
                         zr[k] = (SAFE || (k % kScale == 0)) ? pow2_scale(x, sk[k]) : x;
                     }
                     double gk[kChunk];
@@ -614,11 +633,12 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
                             const int s1 = (k == kChunk - 1) ? s_hi : sk[(k + 1) & (kChunk - 1)];
                             const bool sc1 = SAFE || ((k + 1) % kScale == 0);
                             const double bp = sc1 ? pow2_scale(beta, s1) : beta;
-                            const double vd = e.x * bp;
                             const double vu = dpp<0x101>(e.y * bp);  // row_shl:1
-                            bn = vd + vu;
-                            S[0] = fma(zs, vd, S[0]);  // xi_t(j,j)   (:396-410)
-                            S[1] = fma(zs, vu, S[1]);  // xi_t(j,j+1)
+                            bn = fma(e.x, bp, vu);
+                            // a_jj b_j(o_{t+1}) z_t(j): from the recompute, or (t = 8c+7) one product
+                            const double uk = (k == kChunk - 1) ? e.x * zt : ux[(k + 1) & (kChunk - 1)];
+                            S[0] = fma(reg ? uk : 0.0, bp, S[0]);  // xi_t(j,j)   (:396-410)
+                            S[1] = fma(zs, vu, S[1]);              // xi_t(j,j+1)
                         } else if constexpr (LR) {
                             const double f = (k == kChunk - 1) ? f_hi : fs[k + 1];  // b(o_{t+1}) / c_{t+1}
                             const double fu = (k == kChunk - 1) ? fu_hi : fus[k + 1];
@@ -640,15 +660,17 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
                             bn = b0 + b1;
                         }
                         double g;  // gamma_t(j) (:392)
+                        // PT: sum_{t <= T-2} gamma_t(j) = S_jj + S_j,j+1 (the xi row sums, :431-441),
+                        // formed after the sweep instead of one add per step
                         if constexpr (MASK) {
                             g = reg ? zt * bn : (ini ? zt * inv_p : 0.0);
                             beta = reg ? bn : beta;
-                            gex = fma(zs, bn, gex);
+                            if constexpr (!PT) gex = fma(zs, bn, gex);
                             gall += ini ? g : 0.0;
                         } else {
                             g = zt * bn;
                             beta = bn;
-                            gex += g;
+                            if constexpr (!PT) gex += g;
                         }
                         if (t == 0) pin = g;  // :420
                         gk[k] = g;
@@ -664,7 +686,7 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
 #pragma unroll
                         for (int k = 0; k < kChunk; ++k) {  // :474-485
                             if constexpr (LDSTAB) {
-                                atomicAdd(reinterpret_cast<double *>(reinterpret_cast<char *>(sBn + j) + (sym_of(pkA, k) >> 1)), gk[k]);
+                                atomicAdd(reinterpret_cast<double *>(pent(pkA, k) + kHistOff), gk[k]);  // H.h of o_t
                             } else if (gk[k] != 0.0) {
                                 unsafeAtomicAdd(&accb[a.off_bnum + (long long)sym_of(pkA, k) * N + j], gk[k]);
                             }
@@ -698,6 +720,7 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
                 if (full) backward(std::false_type{}, std::false_type{});
                 else backward(std::false_type{}, std::true_type{});
             }
+            if constexpr (PT) gex = S[0] + S[1];
             gall += gex;
             PHASE(3);
             // xi_t(i,j) = a_ij * (the accumulated S_ij): scale once per sequence group (PT already
@@ -762,7 +785,7 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
             for (int idx = tid; idx < K * G; idx += blockDim.x) {
                 const int k = idx / G, jj = idx - k * G;
                 if (jj >= N) continue;
-                const double x = sBn[k * GP + jj];
+                const double x = sH[((size_t)k * GP + jj) * 2];
                 if (x != 0.0) unsafeAtomicAdd(&accb[a.off_bnum + (long long)k * N + jj], x);
             }
         }
@@ -1128,8 +1151,8 @@ __device__ __forceinline__ double wave_max(double x) {
     return fmax(x, __shfl_xor(x, 32));
 }
 
-template <int N, int G, int GP, bool HIST, bool PT, int BLK>
-__device__ bool merged_mstep(const EArgs &a, double *sBt, double2 *sBP, double *sBn, double *sPA, long long bid) {
+template <int N, int G, int GP, bool PT, int BLK>
+__device__ bool merged_mstep(const EArgs &a, double *sP, double *sH, double *sPA, long long bid) {
     constexpr int NSM = N + N * N + 2 * N;  // pi_num, xi, gamma_den_excl, gamma_den_all
     constexpr int NW = BLK / 64;
     constexpr int SB = kMergedMaxStats / BLK;
@@ -1251,12 +1274,15 @@ __device__ bool merged_mstep(const EArgs &a, double *sBt, double2 *sBP, double *
         const double inv = kSameState ? inv0 : mstep_inv(sSm[N + N * N + N + jj]);
         bval[q] = bnum_to_b(v[q], inv);
         if (e >= 0 && e < K * N) {
-            sBt[(e / N) * GP + jj] = bval[q];
+            const int i = (e / N) * GP + jj;
             if constexpr (PT) {
                 const double ad = kSameState ? ad0 : a_of(jj, jj);
                 const double ai = kSameState ? ai0 : (jj >= 1 ? a_of(jj - 1, jj) : 0.0);
-                sBP[(e / N) * GP + jj] = double2{ad * bval[q], ai * bval[q]};
+                reinterpret_cast<double2 *>(sP)[i] = double2{ad * bval[q], ai * bval[q]};
+            } else {
+                reinterpret_cast<double2 *>(sP)[i] = double2{bval[q], 0.0};
             }
+            reinterpret_cast<double2 *>(sH)[i] = double2{0.0, bval[q]};  // this launch's histogram, b
         }
     }
     if (w0) {
@@ -1270,21 +1296,15 @@ __device__ bool merged_mstep(const EArgs &a, double *sBt, double2 *sBP, double *
             }
         }
     }
-    // zero the pad columns [N, GP) of every row and the pad row K; clear the histogram
+    // zero the pad columns [N, GP) of every row and the pad row K (records and histogram)
     for (int i = tid; i < (K + 1) * (GP - N); i += BLK) {
         const int k = i / (GP - N), c = N + (i - k * (GP - N));
-        sBt[k * GP + c] = 0.0;
-        if constexpr (PT) sBP[k * GP + c] = double2{0.0, 0.0};
+        reinterpret_cast<double2 *>(sP)[k * GP + c] = double2{0.0, 0.0};
+        reinterpret_cast<double2 *>(sH)[k * GP + c] = double2{0.0, 0.0};
     }
     if (tid < N) {
-        sBt[K * GP + tid] = 0.0;
-        if constexpr (PT) sBP[K * GP + tid] = double2{0.0, 0.0};
-    }
-    if constexpr (HIST) {
-        double2 *z2 = reinterpret_cast<double2 *>(sBn);
-        for (int i = tid; i < K * GP / 2; i += BLK) z2[i] = double2{0.0, 0.0};
-        if ((K * GP) & 1)
-            if (tid == 0) sBn[K * GP - 1] = 0.0;
+        reinterpret_cast<double2 *>(sP)[K * GP + tid] = double2{0.0, 0.0};
+        reinterpret_cast<double2 *>(sH)[K * GP + tid] = double2{0.0, 0.0};
     }
     __syncthreads();
     double S = 0.0;

@@ -24,16 +24,6 @@ struct Kernels {
 template <int N>
 Kernels small_kernels_n(bool lr, bool ldstab);
 
-// Dense-A kernels on the fp64 matrix cores for 5 <= N <= 8 (estep_dmfma.hpp): the small layout,
-// 128-thread workgroups; empty Kernels for other N.
-template <int N>
-Kernels dmfma_kernels_n();
-
-// Left-to-right kernels with two states per lane for 5 <= N <= 8 (estep_lr2.hpp): the small layout,
-// 128-thread workgroups; empty Kernels for other N.
-template <int N>
-Kernels lr2_kernels_n();
-
 // Wide kernels (16 < N <= 64) for the padded state count NP (32, 48 or 64).
 Kernels wide_kernels(int NP);
 

@@ -161,17 +161,6 @@ int hmmbw_score(hmmbw_ctx *ctx, double *out);
  * each workgroup straight into its LDS tables (when the emission tables fit LDS); 0: a separate
  * one-workgroup M-step kernel after every E-step. */
 #define HMMBW_OPT_MERGE_MSTEP 4
-/* Dense A with 5 <= N <= 8 on the fp64 matrix cores (16-sequence MFMA tiles, estep_dmfma.hpp):
- * 0 (default) never (the VALU kernel: lane = state, cross-lane broadcasts), 1 for the forward-only
- * scorer, 2 for the scorer and the E-step.  Measured at cfg3 dense (10,000 x 200, N=8): E-step 268
- * vs 162 us (its forward sweep is faster, its backward, one 16-sequence tile per wave with no second
- * wave to hide the MFMA and LDS latencies, is 4.6x slower), scorer no faster, hence off by default.
- * Results agree to fp64 rounding either way (tests/test_gpu_dmfma.py). */
-#define HMMBW_OPT_DENSE_MFMA 5
-/* Left-to-right A with 5 <= N <= 8: 1 runs the two-states-per-lane kernel (16 sequences per wave,
- * estep_lr2.hpp), 0 (default) the one-state-per-lane kernel (8 sequences per wave).  Experimental:
- * parity-green, but measured 1.8x slower at cfg3 (90 vs 50 us per E-step). */
-#define HMMBW_OPT_LR_PAIRS 6
 int hmmbw_set_option(hmmbw_ctx *ctx, int key, int64_t value);
 
 /* E-step kernel timing with HIP events on the context stream (for bench/roofline).  Returns the
