@@ -234,11 +234,11 @@ struct hmmbw_ctx {
     long long stats_len() const { return off_ll() + 2LL * world; }
     long long copy_len() const { return off_ll(); }
     // emission table + B-numerator histogram in LDS ([K][G+1] fp64 each) when they fit 48 KiB
-    // emission P/H tables in LDS (two [K+1][G+1] tables of 16-B entries kHistOff bytes apart, see
+    // emission P/H tables in LDS (two [K][G + kTabPad] tables of 16-B entries kHistOff bytes apart, see
     // hmmbw_device.hpp) when the first fits below kHistOff (the row offsets then fit the uint16 packs)
-    bool lds_tables() const { return !wide && lds_tables_fit(K, G + 1); }
+    bool lds_tables() const { return !wide && lds_tables_fit(K, G + kTabPad); }
     // LDS doubles of the small kernels' tables
-    size_t lds_table_doubles() const { return lds_tables() ? lds_table_bytes(K, G + 1) / sizeof(double) : 0; }
+    size_t lds_table_doubles() const { return lds_tables() ? lds_table_bytes(K, G + kTabPad) / sizeof(double) : 0; }
     bool can_merge() const { return merge_mstep && lds_tables() && copy_len() <= kMergedMaxStats && nwaves > 0; }
     IterState *state() const { return d_state + scur; }
     double *copies(long long e) const { return d_copies + (e % 3) * (long long)ncopies * copy_len(); }
@@ -723,7 +723,7 @@ int hmmbw_set_observations(hmmbw_ctx *c, const int64_t *offsets, const int32_t *
     // packs hold LDS byte offsets of the emission record rows when the tables live in LDS (< 64 KiB,
     // so they fit uint16), symbol ids otherwise
     const bool lds_off = c->lds_tables();
-    const long long row_bytes = (long long)(c->G + 1) * 16;  // 16-B table entries
+    const long long row_bytes = (long long)(c->G + kTabPad) * 16;  // 16-B table entries
     std::vector<uint16_t> hsym((size_t)std::max(symtot, 1LL), 0);
     for (long long w = 0; w < nwaves; ++w)
         for (int u = 0; u < U; ++u) {

@@ -267,17 +267,25 @@ __device__ void block_ll_partial(double lp, bool valid, double *sh, double *out)
 //   gamma_t(i) = z_t(i) beta_hat_t(i),  xi_t(i,j) = a_ij z_t(i) v_j  (accumulated as S_ij = xi/a_ij).
 // gamma is scattered into the per-workgroup LDS histogram B_num[o_t][j] (ds_add_f64).
 // ---------------------------------------------------------------------------------------------
-// LDS emission tables of the small kernels: two [(K + 1) x GP] tables of 16-byte entries, row K zero
-// (the padding symbol of ragged waves), the second kHistOff bytes after the first:
+// LDS emission tables of the small kernels: two [K x GP] tables of 16-byte entries (GP = G + kTabPad
+// columns, the columns past N zero), the second kHistOff bytes after the first:
 //   P-table {x, y}: left-to-right x = a_jj b_j(o), y = a_{j-1,j} b_j(o) (the two products of the
 //                   forward step); dense x = b_j(o), y = 0;
 //   H-table {h, b}: h = the workgroup's B-numerator histogram (hmm_training.py:474-485), b = b_j(o).
 // The symbol packs hold the byte offset of the symbol's row, o * GP * 16, so ONE lane address per step
 // serves the emission read (ds_read_b128, offset 0) and the histogram add (ds_add_f64, offset
 // kHistOff): the constant distance is the instructions' immediate offset.
-constexpr int kHistOff = 40960;
-__host__ __device__ constexpr bool lds_tables_fit(int K, int GP) { return (size_t)(K + 1) * GP * 16 <= (size_t)kHistOff; }
-__host__ __device__ constexpr size_t lds_table_bytes(int K, int GP) { return (size_t)kHistOff + (size_t)(K + 1) * GP * 16; }
+// Rows are 8 x 16 B for G = 8 (no pad column): a ds_read_b128 lane group (4 windows of 4 states of 4
+// sequences) then meets 1.74 bank conflicts per 16 lanes on uniform symbols, against 2.44 with a pad
+// column (simulated with the MI355X_MICROARCH.md grouping; tools/lds_banks.py).  Padding slots of
+// ragged waves read row 0 (any finite entry: their steps are masked and add 0 to the histogram).
+#ifndef HMMBW_TAB_PAD
+#define HMMBW_TAB_PAD 0
+#endif
+constexpr int kTabPad = HMMBW_TAB_PAD;
+constexpr int kHistOff = kTabPad ? 40960 : 32768;
+__host__ __device__ constexpr bool lds_tables_fit(int K, int GP) { return (size_t)K * GP * 16 <= (size_t)kHistOff; }
+__host__ __device__ constexpr size_t lds_table_bytes(int K, int GP) { return (size_t)kHistOff + (size_t)K * GP * 16; }
 
 template <int N, int G, int GP, bool PT, int BLK = kBlock>
 __device__ bool merged_mstep(const EArgs &a, double *sP, double *sH, double *sPA, long long bid);
@@ -290,7 +298,7 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
     constexpr int U = kWave / G;
     constexpr int NS = LR ? 2 : N;      // per-lane S accumulators (row j of S)
     constexpr int NV = NS + 3;          // + gamma_den_excl, gamma_den_all, pi_num
-    constexpr int GP = LDSTAB ? G + 1 : G;  // row stride of the emission / histogram tables
+    constexpr int GP = LDSTAB ? G + kTabPad : G;  // row stride of the emission / histogram tables
     // left-to-right with LDS tables: per (symbol, state) products {a_jj b_j(o), a_{j-1,j} b_j(o)}
     constexpr bool PT = LR && LDSTAB;
     extern __shared__ double smem[];
@@ -302,8 +310,8 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
             a.zero[i] = 0.0;
     const int j = lane & (G - 1), u = lane / G;
     const int K = a.K;
-    double *sP = smem;                   // LDSTAB: P-table [K+1][GP] {x, y} (see kHistOff)
-    double *sH = smem + kHistOff / 8;    // LDSTAB: H-table [K+1][GP] {h, b}
+    double *sP = smem;                   // LDSTAB: P-table [K][GP] {x, y} (see kHistOff)
+    double *sH = smem + kHistOff / 8;    // LDSTAB: H-table [K][GP] {h, b}
     double *sRed = smem + (LDSTAB ? lds_table_bytes(K, GP) / 8 : 0);  // [waves][G][NV] + ll scratch
     bool merged = false;
     if constexpr (LDSTAB && !FWD_ONLY) merged = a.merged != 0;
@@ -320,7 +328,7 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
             if constexpr (PT) __syncthreads();  // the records fold a_jj, a_{j-1,j} in
             // 16 independent loads in flight per thread before the first LDS store
             constexpr int TB = 16;
-            const int nt = (K + 1) * GP;
+            const int nt = K * GP;
             for (int i0 = 0; i0 < nt; i0 += TB * kBlock) {
                 double x[TB];
 #pragma unroll
@@ -461,8 +469,9 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
             Em E[2][kChunk];
 #pragma unroll
             for (int k = 0; k < kChunk; ++k) E[0][k] = ld_em(Q[0], k);
-            auto chunk = [&](int c, const Em (&bv)[kChunk], auto MASK_) {
+            auto chunk = [&](int c, const Em (&bv)[kChunk], auto MASK_, auto FIRST_) {
                 constexpr bool MASK = decltype(MASK_)::value;
+                constexpr bool FIRST = decltype(FIRST_)::value;  // chunk 0: step 0 is pi_j b_j(o_0)
                 const int Tend = RAG ? T : Tw;
                 int sp[kChunk];
 #pragma unroll
@@ -471,13 +480,13 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
                     double zn;
                     int st = 0;
                     if constexpr (SAFE) {
-                        const double x = (t == 0) ? pij * b00 : step(z, bv[k]);
+                        const double x = (FIRST && k == 0) ? pij * b00 : step(z, bv[k]);
                         const int M = group_bexp(x);
                         st = M == 0 ? 0 : M - 1023;
                         zn = pow2_scale(x, st);
                     } else if (k % kScale == 0) {
                         st = pend[k / kScale];
-                        zn = pow2_scale((t == 0) ? pij * b00 : step(z, bv[k]), st);
+                        zn = pow2_scale((FIRST && k == 0) ? pij * b00 : step(z, bv[k]), st);
                         const int M = group_bexp(zn);
                         // applied kScale steps later; clamped so an all-zero (dead) group can never
                         // scale itself to inf (the fallback below catches it)
@@ -503,20 +512,48 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
                 }
                 if constexpr (!FWD_ONLY) spw[(long long)c * U] = pack_exps(sp);
             };
-            auto body = [&](int c, auto R_) {
+            // chunk c uses ring slot r = c % 4.  The steady loop runs 4 chunks per trip with no
+            // branches around loads or stores, so the compiler's s_waitcnt vmcnt counts stay exact
+            // (a conditional chunk makes it wait for every store of the previous chunks).
+            using F0 = std::false_type;
+            using F1 = std::true_type;
+            auto body = [&](int c, auto R_, auto MASK_, auto FIRST_) {
                 constexpr int r = decltype(R_)::value;
+                __builtin_amdgcn_sched_barrier(0);  // one chunk at a time: registers stay per chunk
                 CHUNKSTAMP(0, c);
 #pragma unroll
                 for (int k = 0; k < kChunk; ++k) E[(r + 1) & 1][k] = ld_em(Q[(r + 1) & 3], k);
-                if (c + 4 < nch) Q[r] = loadpack(c + 4);
-                if (RAG || (c == nch - 1 && (Tw % kChunk) != 0)) chunk(c, E[r & 1], std::true_type{});
-                else chunk(c, E[r & 1], std::false_type{});
+                Q[r] = loadpack(c + 4 < nch ? c + 4 : nch - 1);
+                chunk(c, E[r & 1], MASK_, FIRST_);
             };
-            for (int c = 0; c < nch; c += 4) {
-                body(c, std::integral_constant<int, 0>{});
-                if (c + 1 < nch) body(c + 1, std::integral_constant<int, 1>{});
-                if (c + 2 < nch) body(c + 2, std::integral_constant<int, 2>{});
-                if (c + 3 < nch) body(c + 3, std::integral_constant<int, 3>{});
+            auto tail_body = [&](int c, auto R_) {  // masked where the wave's last chunk is partial
+                if (RAG || (c == nch - 1 && (Tw % kChunk) != 0)) body(c, R_, F1{}, F0{});
+                else body(c, R_, F0{}, F0{});
+            };
+            using I0 = std::integral_constant<int, 0>;
+            using I1 = std::integral_constant<int, 1>;
+            using I2 = std::integral_constant<int, 2>;
+            using I3 = std::integral_constant<int, 3>;
+            if (RAG || (nch == 1 && (Tw % kChunk) != 0)) body(0, I0{}, F1{}, F1{});
+            else body(0, I0{}, F0{}, F1{});
+            const int lim = RAG ? nch : ((Tw % kChunk) != 0 ? nch - 1 : nch);  // chunks [1, lim) unmasked (full)
+            int c = 1;
+            using Mk = std::integral_constant<bool, RAG>;
+            for (; c + 4 <= lim; c += 4) {
+                body(c, I1{}, Mk{}, F0{});
+                body(c + 1, I2{}, Mk{}, F0{});
+                body(c + 2, I3{}, Mk{}, F0{});
+                body(c + 3, I0{}, Mk{}, F0{});
+            }
+            if (c < nch) {
+                tail_body(c, I1{});
+                if (c + 1 < nch) {
+                    tail_body(c + 1, I2{});
+                    if (c + 2 < nch) {
+                        tail_body(c + 2, I3{});
+                        if (c + 3 < nch) tail_body(c + 3, I0{});
+                    }
+                }
             }
             return (!SAFE) && (minM < 1023 - 900 || maxM > 1023 + 900);
         };
@@ -700,17 +737,22 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
                 auto body = [&](int c, auto R_, auto MASK_) {
                     constexpr int r = decltype(R_)::value;
                     constexpr int rn = (r + 1) & 3;
+                    __builtin_amdgcn_sched_barrier(0);  // one chunk at a time: registers stay per chunk
                     CHUNKSTAMP(1, c);
                     chunk(c, X[r], X[rn].pk, E[r & 1], BU[r & 1], E[(r + 1) & 1], BU[(r + 1) & 1], MASK_);
-                    if (c >= 4) X[r] = ldset(c - 4);
+                    X[r] = ldset(c >= 4 ? c - 4 : 0);  // branch-free: exact vmcnt accounting
                 };
                 using Mk = std::integral_constant<bool, RAG>;  // only the first chunk is masked in full waves
-                body(cl, std::integral_constant<int, 0>{}, std::true_type{});  // holds t = Tw - 1
+                using I0 = std::integral_constant<int, 0>;
+                using I1 = std::integral_constant<int, 1>;
+                using I2 = std::integral_constant<int, 2>;
+                using I3 = std::integral_constant<int, 3>;
+                body(cl, I0{}, std::true_type{});  // holds t = Tw - 1
                 for (int c = cl - 1; c >= 0; c -= 4) {
-                    body(c, std::integral_constant<int, 1>{}, Mk{});
-                    if (c >= 1) body(c - 1, std::integral_constant<int, 2>{}, Mk{});
-                    if (c >= 2) body(c - 2, std::integral_constant<int, 3>{}, Mk{});
-                    if (c >= 3) body(c - 3, std::integral_constant<int, 0>{}, Mk{});
+                    body(c, I1{}, Mk{});
+                    if (c >= 1) body(c - 1, I2{}, Mk{});
+                    if (c >= 2) body(c - 2, I3{}, Mk{});
+                    if (c >= 3) body(c - 3, I0{}, Mk{});
                 }
             };
             if (safe) {
@@ -794,7 +836,7 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
 }
 
 template <int N, int G, bool LR, bool LDSTAB, bool FWD_ONLY>
-__global__ void __launch_bounds__(kBlock) k_estep_small(EArgs a) {
+__global__ void __launch_bounds__(kBlock, LR ? 2 : 1) k_estep_small(EArgs a) {  // LR: 2 waves per SIMD (<= 256 VGPRs)
     estep_small_body<N, G, LR, LDSTAB, FWD_ONLY>(a, blockIdx.x, gridDim.x);
 }
 
@@ -803,7 +845,7 @@ __global__ void __launch_bounds__(kBlock) k_estep_small(EArgs a) {
 // convergence state).  Replaces the per-word loop of HMM/main.py:147-152 (train) and the per-model
 // loop of HMM/hmm_testing.py:139-161 (test) with one launch per EM iteration / per scoring pass.
 template <int N, int G, bool LR, bool LDSTAB, bool FWD_ONLY>
-__global__ void __launch_bounds__(kBlock) k_estep_small_group(GroupArgs g) {
+__global__ void __launch_bounds__(kBlock, LR ? 2 : 1) k_estep_small_group(GroupArgs g) {
     const long long b = blockIdx.x;
     int lo = 0, hi = g.nm - 1;  // the last model whose first workgroup is <= b (uniform search)
     while (lo < hi) {
@@ -1296,15 +1338,13 @@ __device__ bool merged_mstep(const EArgs &a, double *sP, double *sH, double *sPA
             }
         }
     }
-    // zero the pad columns [N, GP) of every row and the pad row K (records and histogram)
-    for (int i = tid; i < (K + 1) * (GP - N); i += BLK) {
-        const int k = i / (GP - N), c = N + (i - k * (GP - N));
-        reinterpret_cast<double2 *>(sP)[k * GP + c] = double2{0.0, 0.0};
-        reinterpret_cast<double2 *>(sH)[k * GP + c] = double2{0.0, 0.0};
-    }
-    if (tid < N) {
-        reinterpret_cast<double2 *>(sP)[K * GP + tid] = double2{0.0, 0.0};
-        reinterpret_cast<double2 *>(sH)[K * GP + tid] = double2{0.0, 0.0};
+    // zero the pad columns [N, GP) of every row (products, histogram, b)
+    if constexpr (GP > N) {
+        for (int i = tid; i < K * (GP - N); i += BLK) {
+            const int k = i / (GP - N), c = N + (i - k * (GP - N));
+            reinterpret_cast<double2 *>(sP)[k * GP + c] = double2{0.0, 0.0};
+            reinterpret_cast<double2 *>(sH)[k * GP + c] = double2{0.0, 0.0};
+        }
     }
     __syncthreads();
     double S = 0.0;

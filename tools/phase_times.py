@@ -31,9 +31,10 @@ def main():
     a = ap.parse_args()
     out_dir = os.path.join(ROOT, "gpurun_out", "phase")
     os.makedirs(out_dir, exist_ok=True)
-    lib = os.path.join(out_dir, "libhmmbw_phase.so")
-    from hmm_training_amd import build as B
-    B.build(force=True, defines=["-DHMMBW_PHASE_TIMES"], out=lib, tag="phase")
+    lib = os.path.join(ROOT, "hmm_training_amd", "libhmmbw_phase.so")  # prebuilt in-tree if present
+    if not os.path.exists(lib):
+        from hmm_training_amd import build as B
+        B.build(force=True, defines=["-DHMMBW_PHASE_TIMES"], out=lib, tag="phase")
     os.environ["HMMBW_LIB"] = lib
     import torch
     from hmm_training_amd.engine import BaumWelchEngine
