@@ -204,6 +204,44 @@ __device__ __forceinline__ void sfor(F &&f) {
     }
 }
 
+// Dense-A cross-lane products with the broadcast fused into the multiply-add: gfx950's 64-bit DPP
+// ("DP ALU DPP") has only row_newbcast, which broadcasts lane L of every 16-lane row, so for G-lane
+// groups (G = 4, 8, 16) one v_fmac_f64_dpp per group position Q, with bank_mask restricting the write
+// to that group's lanes, gives  acc += z(lane I of this lane's group) * a  in 16 / G instructions, in
+// place of a broadcast, a select and an fma per group (the compiler does not fuse 64-bit DPP moves).
+template <int G, int I, int Q>
+__device__ __forceinline__ void fmac_bcast1(double &acc, double z, double a) {
+    constexpr int lane = Q * G + I;
+    constexpr int bm = ((1 << (G / 4)) - 1) << (Q * G / 4);
+    asm volatile("v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:%4"
+                 : "+v"(acc) : "v"(z), "v"(a), "i"(lane), "i"(bm));
+}
+// VALU write -> DPP read of that VGPR needs 2 wait states; the compiler does not see the DPP read
+// inside the asm, so the first fused product after z is written goes behind this.
+__device__ __forceinline__ void dpp_guard(double z) { asm volatile("s_nop 1" ::"v"(z)); }
+
+// acc0 += sum over even i of a[i] z(lane i), acc1 the odd i (two chains), per G-lane group
+template <int G, int N>
+__device__ __forceinline__ void bcast_dot(double &acc0, double &acc1, double z, const double (&a)[N]) {
+    dpp_guard(z);
+    sfor<0, (N + 1) / 2>([&](auto P) {
+        constexpr int i0 = 2 * decltype(P)::value, i1 = i0 + 1;
+        sfor<0, 16 / G>([&](auto Q) {
+            fmac_bcast1<G, i0, decltype(Q)::value>(acc0, z, a[i0]);
+            if constexpr (i1 < N) fmac_bcast1<G, i1, decltype(Q)::value>(acc1, z, a[i1]);
+        });
+    });
+}
+
+// S[i] += z(lane i) * w for every state i of the group
+template <int G, int N, int NS>
+__device__ __forceinline__ void bcast_acc(double (&S)[NS], double z, double w) {
+    dpp_guard(z);
+    sfor<0, 16 / G>([&](auto Q) {
+        sfor<0, N>([&](auto I) { fmac_bcast1<G, decltype(I)::value, decltype(Q)::value>(S[decltype(I)::value], z, w); });
+    });
+}
+
 __device__ __forceinline__ int sym_of(const uint4 &p, int s) {
     const unsigned w = s < 2 ? p.x : (s < 4 ? p.y : (s < 6 ? p.z : p.w));
     return (s & 1) ? int(w >> 16) : int(w & 0xFFFFu);
@@ -429,11 +467,15 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
             } else {
                 const double bs = e;
                 double acc0 = 0.0, acc1 = 0.0;
-                sfor<0, N>([&](auto I) {
-                    const double zi = gbcast<G, I.value>(zp, lane);
-                    if constexpr ((I.value & 1) == 0) acc0 = fma(acol[I.value], zi, acc0);
-                    else acc1 = fma(acol[I.value], zi, acc1);
-                });
+                if constexpr (G >= 4) {
+                    bcast_dot<G, N>(acc0, acc1, zp, acol);
+                } else {
+                    sfor<0, N>([&](auto I) {
+                        const double zi = gbcast<G, I.value>(zp, lane);
+                        if constexpr ((I.value & 1) == 0) acc0 = fma(acol[I.value], zi, acc0);
+                        else acc1 = fma(acol[I.value], zi, acc1);
+                    });
+                }
                 return (acc0 + acc1) * bs;
             }
         };
@@ -688,12 +730,17 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
                             const double f = (k == kChunk - 1) ? f_hi : fs[k + 1];  // b(o_{t+1}) / c_{t+1}
                             const double vd = f * beta;
                             double b0 = 0.0, b1 = 0.0;
-                            sfor<0, N>([&](auto I) {
-                                const double vk = gbcast<G, I.value>(vd, lane);
-                                if constexpr ((I.value & 1) == 0) b0 = fma(arow[I.value], vk, b0);
-                                else b1 = fma(arow[I.value], vk, b1);
-                                S[I.value] = fma(zs, vk, S[I.value]);   // :402-408
-                            });
+                            if constexpr (G >= 4) {
+                                bcast_dot<G, N>(b0, b1, vd, arow);   // :182-193
+                                bcast_acc<G, N>(S, vd, zs);          // :402-408
+                            } else {
+                                sfor<0, N>([&](auto I) {
+                                    const double vk = gbcast<G, I.value>(vd, lane);
+                                    if constexpr ((I.value & 1) == 0) b0 = fma(arow[I.value], vk, b0);
+                                    else b1 = fma(arow[I.value], vk, b1);
+                                    S[I.value] = fma(zs, vk, S[I.value]);   // :402-408
+                                });
+                            }
                             bn = b0 + b1;
                         }
                         double g;  // gamma_t(j) (:392)
@@ -719,16 +766,19 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
                     // next chunk's emission rows go to LDS before this chunk's histogram atomics, so
                     // they are not queued behind them
                     ldrows(bvn, bun, pkn);
-                    if ((N == G || jv) && !(a.ablate & 4)) {
+#ifndef HMMBW_NO_HIST  // diagnostics build: no B-numerator histogram
+                    if constexpr (LDSTAB) {
+                        // every lane, no branch (the pad lanes j >= N add their zero gamma to the pad
+                        // columns), so the compiler's lgkmcnt bookkeeping stays exact
 #pragma unroll
-                        for (int k = 0; k < kChunk; ++k) {  // :474-485
-                            if constexpr (LDSTAB) {
-                                atomicAdd(reinterpret_cast<double *>(pent(pkA, k) + kHistOff), gk[k]);  // H.h of o_t
-                            } else if (gk[k] != 0.0) {
-                                unsafeAtomicAdd(&accb[a.off_bnum + (long long)sym_of(pkA, k) * N + j], gk[k]);
-                            }
-                        }
+                        for (int k = 0; k < kChunk; ++k)  // :474-485
+                            atomicAdd(reinterpret_cast<double *>(pent(pkA, k) + kHistOff), gk[k]);  // H.h of o_t
+                    } else if (N == G || jv) {
+#pragma unroll
+                        for (int k = 0; k < kChunk; ++k)
+                            if (gk[k] != 0.0) unsafeAtomicAdd(&accb[a.off_bnum + (long long)sym_of(pkA, k) * N + j], gk[k]);
                     }
+#endif
                     if constexpr (!PT) {
                         f_hi = fs[0];
                         if constexpr (LR) fu_hi = fus[0];
@@ -748,11 +798,30 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
                 using I2 = std::integral_constant<int, 2>;
                 using I3 = std::integral_constant<int, 3>;
                 body(cl, I0{}, std::true_type{});  // holds t = Tw - 1
-                for (int c = cl - 1; c >= 0; c -= 4) {
-                    body(c, I1{}, Mk{});
-                    if (c >= 1) body(c - 1, I2{}, Mk{});
-                    if (c >= 2) body(c - 2, I3{}, Mk{});
-                    if (c >= 3) body(c - 3, I0{}, Mk{});
+                if constexpr (LDSTAB) {
+                    // steady loop: 4 chunks per trip, no branches around the loads or the LDS
+                    // atomics, so the compiler's vmcnt / lgkmcnt waits stay exact
+                    int c = cl - 1;
+                    for (; c >= 3; c -= 4) {
+                        body(c, I1{}, Mk{});
+                        body(c - 1, I2{}, Mk{});
+                        body(c - 2, I3{}, Mk{});
+                        body(c - 3, I0{}, Mk{});
+                    }
+                    if (c >= 0) {
+                        body(c, I1{}, Mk{});
+                        if (c >= 1) {
+                            body(c - 1, I2{}, Mk{});
+                            if (c >= 2) body(c - 2, I3{}, Mk{});
+                        }
+                    }
+                } else {  // global histogram atomics (skipped for zero gamma): the compact loop
+                    for (int c = cl - 1; c >= 0; c -= 4) {
+                        body(c, I1{}, Mk{});
+                        if (c >= 1) body(c - 1, I2{}, Mk{});
+                        if (c >= 2) body(c - 2, I3{}, Mk{});
+                        if (c >= 3) body(c - 3, I0{}, Mk{});
+                    }
                 }
             };
             if (safe) {
