@@ -7,21 +7,28 @@ SRC=gpurun_out/prof_$TAG
 mkdir -p "profiles/$DEST"
 cp "$SRC/calib_FETCH_SIZE/run_counter_collection.csv" "profiles/$DEST/pmc_calib_FETCH_SIZE.csv"
 cp "$SRC/calib_WRITE_SIZE/run_counter_collection.csv" "profiles/$DEST/pmc_calib_WRITE_SIZE.csv"
-for TOPO in left_to_right dense; do
-  cp "$SRC/trace_$TOPO/run_kernel_stats.csv" "profiles/$DEST/kernel_stats_${TOPO}_cfg3.csv"
-  for C in FETCH_SIZE WRITE_SIZE; do
-    cp "$SRC/pmc_${C}_$TOPO/run_counter_collection.csv" "profiles/$DEST/pmc_${C}_${TOPO}_cfg3.csv"
+declare -A KEY=([lr_cfg3]=R10000_T200_N8_K256_left_to_right [lrH_cfg3]=R10000_T200_N8_K256_left_to_right_H
+                [dense_cfg3]=R10000_T200_N8_K256_dense [cfg5]=R6250_T400_N64_K1024_dense)
+declare -A KER=([lr_cfg3]=k_estep_small [lrH_cfg3]=k_estep_small [dense_cfg3]=k_estep_small
+                [cfg5]="k_estep_mfma,k_bnum_gather")
+for W in lr_cfg3 lrH_cfg3 dense_cfg3 cfg5; do
+  cp "$SRC/trace_$W/run_kernel_stats.csv" "profiles/$DEST/kernel_stats_$W.csv"
+  for C in FETCH_SIZE WRITE_SIZE SQ; do
+    cp "$SRC/pmc_${C}_$W/run_counter_collection.csv" "profiles/$DEST/pmc_${C}_$W.csv"
   done
-  python3 tools/traffic_summary.py --fetch "profiles/$DEST/pmc_FETCH_SIZE_${TOPO}_cfg3.csv" \
-    --write "profiles/$DEST/pmc_WRITE_SIZE_${TOPO}_cfg3.csv" \
+  python3 tools/traffic_summary.py --fetch "profiles/$DEST/pmc_FETCH_SIZE_$W.csv" \
+    --write "profiles/$DEST/pmc_WRITE_SIZE_$W.csv" \
     --calib-fetch "profiles/$DEST/pmc_calib_FETCH_SIZE.csv" --calib-write "profiles/$DEST/pmc_calib_WRITE_SIZE.csv" \
-    --kernel k_estep_small --config-key "R10000_T200_N8_K256_$TOPO" --out "profiles/$DEST/traffic_${TOPO}_cfg3.json"
+    --kernel "${KER[$W]}" --config-key "${KEY[$W]}" --out "profiles/$DEST/traffic_$W.json"
+  python3 tools/pmc_summary.py "profiles/$DEST/pmc_SQ_$W.csv" "${KER[$W]}" > "profiles/$DEST/sq_$W.json"
 done
-for W in cfg5 cfg2 vq; do
+for W in cfg2 vq; do
   cp "$SRC/trace_$W/run_kernel_stats.csv" "profiles/$DEST/kernel_stats_$W.csv"
 done
 grep -h '"metric"' "$SRC/bench_full.log" > "profiles/$DEST/bench_lr_cfg3.json"
 grep -h '"metric"' "$SRC/bench_dense.log" > "profiles/$DEST/bench_dense_cfg3.json"
+grep -h '"metric"' "$SRC/bench_H.log" > "profiles/$DEST/bench_lrH_cfg3.json"
 grep -h '"metric"' "$SRC/bench_cfg5.log" > "profiles/$DEST/bench_cfg5.json"
+grep -h '"metric"' "$SRC/bench_cfg4shard.log" > "profiles/$DEST/bench_cfg4shard.json"
 grep -h '"workload"' "$SRC/bench_cfg2_full.log" > "profiles/$DEST/bench_cfg2_grouped.json"
 grep -h '"kernel"' "$SRC/bench_vq.log" > "profiles/$DEST/bench_vq.json"

@@ -80,6 +80,8 @@ def main():
     l.hmmbw_debug_chunk_times.argtypes = [ctypes.c_void_p, ctypes.c_int64]
     assert l.hmmbw_debug_chunk_times(ck.ctypes.data, nw_pad) == 0
     ck = ck[:nw].astype(np.int64)
+    if not np.any(ck):
+        return  # chunk stamps need -DHMMBW_CHUNK_TIMES as well
     nch = (T + 7) // 8
     fwd = np.diff(ck[:, 0, :nch], axis=1)
     bwd = -np.diff(ck[:, 1, :nch], axis=1)  # stamped in descending chunk order

@@ -1,11 +1,38 @@
-"""Average per-dispatch PMC values of one kernel from tools/pmc_sq.sh output directories."""
-import csv, glob, sys, collections
-root, kern = sys.argv[1], sys.argv[2]
-vals = collections.defaultdict(list)
-for f in glob.glob(f"{root}/p*/run_counter_collection.csv"):
-    for r in csv.DictReader(open(f)):
-        if kern in r["Kernel_Name"]:
-            vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
-for k in sorted(vals):
-    v = vals[k]
-    print(f"{k:28s} {sum(v)/len(v):16.1f}  (n={len(v)})")
+"""Average per-dispatch PMC values of the named kernels from a rocprofv3 counter_collection CSV (or a
+tools/pmc_sq.sh output directory), as JSON, with the derived LDS bank-conflict rate
+(SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE: extra cycles / all LDS-array cycles, MI355X_MICROARCH.md §LDS)
+and VALU / LDS instructions per wave.
+
+    python tools/pmc_summary.py <csv or dir> <kernel substring[,substring...]>
+"""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+
+def main(src, kernels):
+    files = [src] if os.path.isfile(src) else glob.glob(f"{src}/p*/run_counter_collection.csv")
+    out = {}
+    for kern in kernels.split(","):
+        vals = collections.defaultdict(list)
+        for f in files:
+            for r in csv.DictReader(open(f)):
+                if kern in r["Kernel_Name"]:
+                    vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
+        d = {k: sum(v) / len(v) for k, v in sorted(vals.items())}
+        if d.get("SQ_LDS_IDX_ACTIVE"):
+            d["lds_bank_conflict_fraction"] = d.get("SQ_LDS_BANK_CONFLICT", 0.0) / d["SQ_LDS_IDX_ACTIVE"]
+        if d.get("SQ_WAVES"):
+            for c in ("SQ_INSTS_VALU", "SQ_INSTS_LDS"):
+                if c in d:
+                    d[c.lower() + "_per_wave"] = d[c] / d["SQ_WAVES"]
+        d["dispatches"] = max((len(v) for v in vals.values()), default=0)
+        out[kern] = d
+    print(json.dumps(out, indent=2))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2])

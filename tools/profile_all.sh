@@ -1,10 +1,11 @@
 #!/bin/bash
 # Refresh every profile of one round on the GPU box (run from the repo root):
 #   bash tools/profile_all.sh <tag>
-# rocprofv3 kernel trace + stats per workload, then one PMC pass per counter for the headline
-# (never combined with a trace domain), the PMC calibration program, and the bench JSON lines.
+# rocprofv3 kernel trace + stats per workload, then separate PMC passes (never combined with a
+# trace domain): FETCH_SIZE, WRITE_SIZE (HBM traffic, corrected by the tools/pmc_calib.hip run) and an
+# SQ/LDS pass (bank conflicts, VALU/LDS instruction counts), plus the bench JSON lines.
 set -uo pipefail
-TAG=${1:-r1}
+TAG=${1:-r2}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
@@ -16,17 +17,24 @@ for C in FETCH_SIZE WRITE_SIZE; do
   step calib $C
   timeout -k 10 120 rocprofv3 --pmc $C --output-format csv -d "$OUT/calib_$C" -o run -- "$OUT/pmc_calib" > "$OUT/calib_$C.log" 2>&1 || exit 1
 done
-for TOPO in left_to_right dense; do
-  BENCH="$R/bench.py --steps 50 --warmup 5 --no-cpu-baseline --topology $TOPO"
-  step trace $TOPO
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace_$TOPO" -o run -- python3 $BENCH > "$OUT/bench_trace_$TOPO.log" 2>&1 || exit 1
+SQ="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_BUSY_CYCLES SQ_WAVE_CYCLES"
+declare -A ARGS=(
+  [lr_cfg3]="--steps 20 --warmup 3 --no-cpu-baseline --no-synced"
+  [lrH_cfg3]="--steps 20 --warmup 3 --no-cpu-baseline --no-synced --symbols H"
+  [dense_cfg3]="--steps 20 --warmup 3 --no-cpu-baseline --no-synced --topology dense"
+  [cfg5]="--steps 5 --warmup 2 --no-cpu-baseline --no-synced --workload cfg5"
+)
+for W in lr_cfg3 lrH_cfg3 dense_cfg3 cfg5; do
+  BENCH="$R/bench.py ${ARGS[$W]}"
+  step trace $W
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace_$W" -o run -- python3 $BENCH > "$OUT/bench_trace_$W.log" 2>&1 || exit 1
   for C in FETCH_SIZE WRITE_SIZE; do
-    step pmc $C $TOPO
-    timeout -k 10 300 rocprofv3 --pmc $C --output-format csv -d "$OUT/pmc_${C}_$TOPO" -o run -- python3 $BENCH > "$OUT/bench_pmc_${C}_$TOPO.log" 2>&1 || exit 1
+    step pmc $C $W
+    timeout -k 10 300 rocprofv3 --pmc $C --output-format csv -d "$OUT/pmc_${C}_$W" -o run -- python3 $BENCH > "$OUT/bench_pmc_${C}_$W.log" 2>&1 || exit 1
   done
+  step pmc SQ $W
+  timeout -k 10 300 rocprofv3 --pmc $SQ --output-format csv -d "$OUT/pmc_SQ_$W" -o run -- python3 $BENCH > "$OUT/bench_pmc_SQ_$W.log" 2>&1 || exit 1
 done
-step trace cfg5
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace_cfg5" -o run -- python3 $R/bench.py --N 64 --K 1024 --T 400 --R 6250 --steps 10 --warmup 2 --topology dense --no-cpu-baseline > "$OUT/bench_cfg5.log" 2>&1 || exit 1
 step trace cfg2
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace_cfg2" -o run -- python3 $R/tools/bench_cfg2.py --no-cpu > "$OUT/bench_cfg2.log" 2>&1 || exit 1
 step trace vq
@@ -34,5 +42,8 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/
 step bench
 timeout -k 10 300 python3 "$R/bench.py" > "$OUT/bench_full.log" 2>&1 || exit 1
 timeout -k 10 300 python3 "$R/bench.py" --topology dense --no-cpu-baseline > "$OUT/bench_dense.log" 2>&1 || exit 1
+timeout -k 10 300 python3 "$R/bench.py" --symbols H --no-cpu-baseline > "$OUT/bench_H.log" 2>&1 || exit 1
+timeout -k 10 300 python3 "$R/bench.py" --workload cfg5 --steps 10 --warmup 2 --no-cpu-baseline > "$OUT/bench_cfg5.log" 2>&1 || exit 1
+timeout -k 10 300 python3 "$R/bench.py" --workload cfg4 --no-cpu-baseline > "$OUT/bench_cfg4shard.log" 2>&1 || exit 1
 timeout -k 10 300 python3 "$R/tools/bench_cfg2.py" > "$OUT/bench_cfg2_full.log" 2>&1 || exit 1
 step done

@@ -20,6 +20,11 @@ def per_kernel(path, name_sub, counter):
     return vals
 
 
+def per_launch(path, names, counter):
+    """Mean per launch of the E-step, summed over its kernels (comma-separated substrings)."""
+    return sum(mean(per_kernel(path, n, counter)) for n in names.split(","))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--fetch", required=True)
@@ -35,12 +40,14 @@ def main():
     # calibration: KiB reported per known byte count, 8-B-per-lane access (k_read8 / k_write8)
     cf = a.calib_bytes / (mean(per_kernel(a.calib_fetch, "k_read8", "FETCH_SIZE")) * kib)
     cw = a.calib_bytes / (mean(per_kernel(a.calib_write, "k_write8", "WRITE_SIZE")) * kib)
-    f = per_kernel(a.fetch, a.kernel, "FETCH_SIZE")
-    w = per_kernel(a.write, a.kernel, "WRITE_SIZE")
-    rd = mean(f) * kib * cf
-    wr = mean(w) * kib * cw
-    out = {"kernel": a.kernel, "config_key": a.config_key, "launches": [len(f), len(w)],
-           "fetch_size_kib_mean": mean(f), "write_size_kib_mean": mean(w),
+    f = per_launch(a.fetch, a.kernel, "FETCH_SIZE")
+    w = per_launch(a.write, a.kernel, "WRITE_SIZE")
+    rd = f * kib * cf
+    wr = w * kib * cw
+    out = {"kernel": a.kernel, "config_key": a.config_key,
+           "launches": [len(per_kernel(a.fetch, a.kernel.split(",")[0], "FETCH_SIZE")),
+                        len(per_kernel(a.write, a.kernel.split(",")[0], "WRITE_SIZE"))],
+           "fetch_size_kib_mean": f, "write_size_kib_mean": w,
            "calibration": {"fetch_factor": cf, "write_factor": cw, "access": "8 B per lane, 1 GiB streams"},
            "hbm_read_bytes_per_launch": rd, "hbm_write_bytes_per_launch": wr,
            "hbm_bytes_per_launch": rd + wr,
