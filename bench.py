@@ -88,6 +88,7 @@ def parse(argv=None):
     p.add_argument("--seed", type=int, default=None)
     p.add_argument("--no-kernel-timing", action="store_true", help="skip the HIP events")
     p.add_argument("--timing-every", type=int, default=5, help="time every k-th E-step launch")
+    p.add_argument("--deterministic", action="store_true", help="fixed-order reductions (no fp atomics), bitwise reproducible")
     p.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) on MI355X; gloo only for tests")
     p.add_argument("--dry-run", action="store_true", help="launcher + rendezvous + timing skeleton, no GPU work")
     return p.parse_args(argv)
@@ -294,7 +295,8 @@ def main(argv=None):
     offsets = np.arange(R + 1, dtype=np.int64) * T
     pi, A, B = init_params(N, K, topo, np.random.default_rng(seed))
 
-    eng = BaumWelchEngine(N, K, device=device, topology=topo, rank=rank, world_size=world)
+    eng = BaumWelchEngine(N, K, device=device, topology=topo, rank=rank, world_size=world,
+                          deterministic=args.deterministic)
     t_up = time.perf_counter()
     eng.set_observations(offsets=offsets, symbols=symbols, n_seq_global=R * world)
     eng.set_params(pi, A, B)
@@ -374,7 +376,7 @@ def main(argv=None):
             "config": {"workload": f"{wl}: R={R} sequences per GPU ({R * world} total) x T={T}, N={N} states, "
                                    f"K={K} symbols, {topo} A, symbols {args.symbols}, one EM iteration per step",
                        "sequences_per_gpu": R, "sequences_total": R * world, "T": T, "N": N, "K": K,
-                       "topology": topo, "symbols": args.symbols,
+                       "topology": topo, "symbols": args.symbols, "deterministic": bool(args.deterministic),
                        "parallelism": f"dp{world}" if world > 1 else "single",
                        "allreduce": ("rccl (engine communicator, engine stream)" if eng.native_comm else
                                      f"torch.distributed ({args.dist_backend})") if world > 1 else None},

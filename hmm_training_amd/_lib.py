@@ -41,6 +41,7 @@ OPT_SAFE_SCALING = 1
 OPT_ABLATE = 2
 OPT_STAT_COPIES = 3
 OPT_MERGE_MSTEP = 4
+OPT_DETERMINISTIC = 7
 
 
 class HMMBWError(RuntimeError):

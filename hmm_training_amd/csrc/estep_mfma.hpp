@@ -375,8 +375,9 @@ __global__ void __launch_bounds__(NT * 64, 2) k_estep_mfma(EArgs a) {  // 2 wave
 // whose symbol is k.  One workgroup per symbol; its 4 waves take every 4th position of the symbol's
 // list (rows[ptr[k] .. ptr[k+1]), row indices into the gamma buffer, NP doubles each, bt_col order),
 // lane = column; fixed summation order, plain stores into the symbol-major [K][N] statistics block.
+// (also the small kernels' deterministic mode: NP = G columns in state order, perm = 0)
 __global__ void __launch_bounds__(256) k_bnum_gather(const double *gam, const unsigned *rows, const long long *ptr,
-                                                      int NP, int N, double *bnum, const IterState *state) {
+                                                      int NP, int N, int perm, double *bnum, const IterState *state) {
     __shared__ double sh[4][64];
     if (state != nullptr && state->done) return;
     const int k = blockIdx.x, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -401,7 +402,7 @@ __global__ void __launch_bounds__(256) k_bnum_gather(const double *gam, const un
     __syncthreads();
     if (wv == 0 && lane < NP) {
         const double v = (sh[0][lane] + sh[1][lane]) + (sh[2][lane] + sh[3][lane]);
-        const int j = bt_col(lane);  // bt_col is an involution: column -> state
+        const int j = perm ? bt_col(lane) : lane;  // bt_col is an involution: column -> state
         if (j < N) bnum[(long long)k * N + j] = v;
     }
 }

@@ -15,12 +15,14 @@ Kernels small_kernels_n<HMMBW_INST_N>(bool lr, bool ldstab) {
     if (lr) {
         if (ldstab)
             return Kernels{k_estep_small<N, G, true, true, false>, k_estep_small<N, G, true, true, true>,
-                           k_estep_small_group<N, G, true, true, false>, k_estep_small_group<N, G, true, true, true>};
+                           k_estep_small_group<N, G, true, true, false>, k_estep_small_group<N, G, true, true, true>,
+                           k_estep_small<N, G, true, true, false, true>};
         return Kernels{k_estep_small<N, G, true, false, false>, k_estep_small<N, G, true, false, true>};
     }
     if (ldstab)
         return Kernels{k_estep_small<N, G, false, true, false>, k_estep_small<N, G, false, true, true>,
-                       k_estep_small_group<N, G, false, true, false>, k_estep_small_group<N, G, false, true, true>};
+                       k_estep_small_group<N, G, false, true, false>, k_estep_small_group<N, G, false, true, true>,
+                       k_estep_small<N, G, false, true, false, true>};
     return Kernels{k_estep_small<N, G, false, false, false>, k_estep_small<N, G, false, false, true>};
 }
 

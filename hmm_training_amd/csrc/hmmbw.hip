@@ -67,6 +67,17 @@ __global__ void __launch_bounds__(256) k_reduce_local(double *copies, int ncopie
     }
 }
 
+// Deterministic mode: sum the per-workgroup partial statistics [blocks][n] in workgroup order.
+__global__ void __launch_bounds__(256) k_det_reduce(const double *part, long long nblocks, long long n, double *out,
+                                                    const IterState *state) {
+    if (state->done) return;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+        double v = 0.0;
+        for (long long b = 0; b < nblocks; ++b) v += part[b * n + i];
+        out[i] = v;
+    }
+}
+
 __global__ void __launch_bounds__(256) k_mstep(MArgs m) {
     if (carry_if_done(m)) return;
     mstep_block<false>(m);
@@ -180,6 +191,8 @@ struct hmmbw_ctx {
     double *d_copies = nullptr;   // [3][ncopies][copy_len] E-step accumulators (iteration e uses e % 3)
     int ncopies = 2;              // HMMBW_OPT_STAT_COPIES default: halves the flush atomics per address (measured -3 %)
     bool merge_mstep = true;      // run each M-step in the prologue of the next E-step launch
+    bool det = false;             // HMMBW_OPT_DETERMINISTIC: no floating-point atomics (small kernels, LDS tables)
+    double *d_part = nullptr;     // det: per-workgroup partial statistics [blocks][off_bnum]
     bool armed = false;
     long long e_count = 0;        // E-step launches since the statistics were last cleared
     // an M-step whose statistics are ready but which has not run yet (it runs in the next merged
@@ -210,6 +223,12 @@ struct hmmbw_ctx {
     // native RCCL communicator (hmmbw_comm_init): the multi-rank hmmbw_iterate all-reduces d_ext
     ncclComm_t comm = nullptr;
     double *d_ext = nullptr;
+    // fused native path (small kernels): the E-step accumulates straight into a triple-buffered
+    // all-reduce buffer [3][xlen] = {ncopies statistics copies, (max, sum exp) per rank}; the last
+    // workgroup of each launch writes the rank's pair (d_ctr: completion counter)
+    double *d_xbuf = nullptr;
+    long long xlen = 0;
+    int *d_ctr = nullptr;
     // all-reduce timing (hmmbw_comm_info): event pairs around ncclAllReduce, same schedule as timing
     long long ar_seq = 0;
     std::vector<hipEvent_t> ar_free, ar_pending;
@@ -256,7 +275,7 @@ void free_obs(hmmbw_ctx *c) {
     dfree(c->d_sym); dfree(c->d_wsym); dfree(c->d_wckoff); dfree(c->d_wspoff);
     dfree(c->d_wT); dfree(c->d_wfull); dfree(c->d_slen); dfree(c->d_sseq);
     dfree(c->d_ck); dfree(c->d_sp); dfree(c->d_ebuf); dfree(c->d_logp); dfree(c->d_llpart);
-    dfree(c->d_gam); dfree(c->d_bptr); dfree(c->d_brows);
+    dfree(c->d_gam); dfree(c->d_bptr); dfree(c->d_brows); dfree(c->d_part);
     c->has_obs = false;
 }
 
@@ -279,6 +298,7 @@ EArgs make_eargs(hmmbw_ctx *c) {
     a.Bt = c->d_Bt;
     a.ckpt = c->d_ck;
     a.gam = c->d_gam;
+    a.part = c->d_part;
     a.spack = c->d_sp;
     a.ebuf = c->d_ebuf;
     a.copies = c->copies(0);
@@ -303,7 +323,7 @@ EArgs make_eargs(hmmbw_ctx *c) {
 MArgs make_margs(hmmbw_ctx *c, const hmmbw_ctx::Pending &p) {
     MArgs m{};
     m.src = p.src;
-    m.zero_ll = p.local ? nullptr : p.ext + c->off_ll();
+    m.zero_ll = p.local ? nullptr : const_cast<double *>(p.ll);
     m.nsrc = p.nsrc;
     m.copy_len = c->copy_len();
     m.pi = c->d_pi;
@@ -373,7 +393,7 @@ struct Plan {
 // E-step launch e accumulates into copies and llpart; it clears `zero` (zero_len doubles) and, when
 // `merge` is set, first runs the pending M-step in its prologue (which consumes c->pend).
 int plan_estep(hmmbw_ctx *c, bool fwd_only, const IterState *state, double *copies, double *llpart, double *zero,
-               long long zero_len, bool merge, Plan *P) {
+               long long zero_len, bool merge, Plan *P, double *rank_ll = nullptr) {
     Plan &p = *P;
     p = Plan{};
     EArgs &a = p.a;
@@ -383,6 +403,8 @@ int plan_estep(hmmbw_ctx *c, bool fwd_only, const IterState *state, double *copi
     if (llpart) a.llpart = llpart;
     a.zero = zero;
     a.zero_len = zero ? zero_len : 0;
+    a.rank_ll = rank_ll;
+    a.done_ctr = c->d_ctr;
     const int wpb = kBlock / kWave;
     p.grid = (unsigned)c->nblocks;
     if (c->wide) {
@@ -400,8 +422,8 @@ int plan_estep(hmmbw_ctx *c, bool fwd_only, const IterState *state, double *copi
         {
             Kernels ks = lr ? (lds_tab ? pick_small_n<true, true>(c->N) : pick_small_n<true, false>(c->N))
                             : (lds_tab ? pick_small_n<false, true>(c->N) : pick_small_n<false, false>(c->N));
-            p.fn = fwd_only ? ks.score : ks.estep;
-            p.gfn = fwd_only ? ks.group_score : ks.group_estep;
+            p.fn = fwd_only ? ks.score : (c->det ? ks.det_estep : ks.estep);
+            p.gfn = fwd_only ? ks.group_score : (c->det ? nullptr : ks.group_estep);
             if (!p.fn) return fail(HMMBW_E_UNSUPPORTED, "no kernel for N");
             const int NV = (lr ? 2 : c->N) + 3;
             const size_t tabs = c->lds_table_doubles();
@@ -418,9 +440,10 @@ int plan_estep(hmmbw_ctx *c, bool fwd_only, const IterState *state, double *copi
 }
 
 int launch_estep(hmmbw_ctx *c, bool fwd_only, const IterState *state, double *copies = nullptr,
-                 double *llpart = nullptr, double *zero = nullptr, long long zero_len = 0, bool merge = false) {
+                 double *llpart = nullptr, double *zero = nullptr, long long zero_len = 0, bool merge = false,
+                 double *rank_ll = nullptr) {
     Plan p;
-    if (int rc = plan_estep(c, fwd_only, state, copies, llpart, zero, zero_len, merge, &p)) return rc;
+    if (int rc = plan_estep(c, fwd_only, state, copies, llpart, zero, zero_len, merge, &p, rank_ll)) return rc;
     if (p.grid == 0) return HMMBW_OK;
     const EArgs &a = p.a;
     hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -439,7 +462,14 @@ int launch_estep(hmmbw_ctx *c, bool fwd_only, const IterState *state, double *co
     if (int rc = launch_lds(p.fn, p.grid, p.lds, c->stream, a, p.block)) return rc;
     if (c->wide && !fwd_only) {  // B numerator: per-symbol gather of the gamma rows (estep_mfma.hpp)
         hipLaunchKernelGGL(bnum_gather_kernel(), dim3((unsigned)c->K), dim3(256), 0, c->stream, c->d_gam,
-                           c->d_brows, c->d_bptr, c->NP, c->N, a.copies + c->off_bnum(), a.state);
+                           c->d_brows, c->d_bptr, c->NP, c->N, 1, a.copies + c->off_bnum(), a.state);
+        HIP_TRY(hipGetLastError());
+    } else if (c->det && !fwd_only) {  // deterministic mode: fixed-order sums of the partials and gamma rows
+        const long long n = c->off_bnum();
+        hipLaunchKernelGGL(k_det_reduce, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, c->stream, c->d_part,
+                           (long long)p.grid, n, a.copies, a.state);
+        hipLaunchKernelGGL(bnum_gather_kernel(), dim3((unsigned)c->K), dim3(256), 0, c->stream, c->d_gam,
+                           c->d_brows, c->d_bptr, c->G, c->N, 0, a.copies + c->off_bnum(), a.state);
         HIP_TRY(hipGetLastError());
     }
     if (p.flip) c->scur ^= 1;
@@ -592,6 +622,11 @@ int hmmbw_ctx_create(int device, int n_states, int n_symbols, hmmbw_ctx **out) {
     if (!rc) rc = dalloc(&c->d_out, (size_t)c->N + (size_t)c->N * c->N + (size_t)c->N * c->K);
     if (!rc) rc = dalloc(&c->d_state, 2);
     if (!rc) rc = dalloc(&c->d_hist, 2 * (size_t)kHist);
+    if (!rc) rc = dalloc(&c->d_ctr, 1);
+    if (!rc) {
+        const hipError_t e = hipMemset(c->d_ctr, 0, sizeof(int));
+        if (e != hipSuccess) rc = fail(HMMBW_E_HIP, std::string("init: ") + hipGetErrorString(e));
+    }
     if (!rc) rc = realloc_stats(c);
     if (!rc) {
         hipLaunchKernelGGL(k_init_state, dim3(1), dim3(1), 0, c->stream, c->d_state, 0.0, 0LL);
@@ -613,7 +648,7 @@ int hmmbw_ctx_destroy(hmmbw_ctx *c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     else (void)hipDeviceSynchronize();
     dfree(c->d_pi); dfree(c->d_A); dfree(c->d_B); dfree(c->d_Bt); dfree(c->d_out);
-    dfree(c->d_state); dfree(c->d_hist); dfree(c->d_copies); dfree(c->d_ext);
+    dfree(c->d_state); dfree(c->d_hist); dfree(c->d_copies); dfree(c->d_ext); dfree(c->d_xbuf); dfree(c->d_ctr);
     if (c->comm) {
         Rccl *r = nullptr;
         if (rccl_load(nullptr, &r) == HMMBW_OK) (void)r->comm_destroy(c->comm);
@@ -772,12 +807,32 @@ int hmmbw_set_observations(hmmbw_ctx *c, const int64_t *offsets, const int32_t *
         if (!rc) rc = dalloc(&c->d_gam, (size_t)std::max(cktot, 1LL));
         if (!rc) rc = dalloc(&c->d_bptr, bptr.size());
         if (!rc) rc = dalloc(&c->d_brows, brows.size());
+    } else if (c->det) {  // deterministic mode: symbol -> pack positions (gamma row = pack index), stable
+        if (symtot >= (1LL << 32)) return fail(HMMBW_E_UNSUPPORTED, "too many positions for the deterministic mode");
+        bptr.assign((size_t)c->K + 1, 0);
+        for (int64_t i = 0; i < total; ++i) ++bptr[(size_t)symbols[i] + 1];
+        for (int k = 0; k < c->K; ++k) bptr[(size_t)k + 1] += bptr[(size_t)k];
+        std::vector<long long> fill(bptr.begin(), bptr.end() - 1);
+        brows.resize((size_t)std::max<int64_t>(total, 1));
+        for (long long w = 0; w < nwaves; ++w)
+            for (int u = 0; u < U; ++u) {
+                const long long sl = w * U + u;
+                if (sl >= R) continue;
+                const int64_t r = perm[(size_t)sl];
+                for (int t = 0; t < len[(size_t)r]; ++t)
+                    brows[(size_t)fill[(size_t)symbols[offsets[r] + t]]++] =
+                        (unsigned)(wsym[(size_t)w] + ((long long)(t / kChunk) * U + u) * kChunk + t % kChunk);
+            }
+        if (!rc) rc = dalloc(&c->d_gam, (size_t)std::max(symtot, 1LL) * c->G);
+        if (!rc) rc = dalloc(&c->d_bptr, bptr.size());
+        if (!rc) rc = dalloc(&c->d_brows, brows.size());
+        if (!rc) rc = dalloc(&c->d_part, (size_t)std::max(nblocks, 1LL) * (size_t)c->off_bnum());
     }
     if (!rc) rc = dalloc(&c->d_logp, (size_t)std::max<int64_t>(R, 1));
     if (!rc) rc = dalloc(&c->d_llpart, 4 * (size_t)std::max(nblocks, 1LL));
     if (rc) return rc;
     HIP_TRY(hipMemcpy(c->d_sym, hsym.data(), sizeof(uint16_t) * hsym.size(), hipMemcpyHostToDevice));
-    if (c->wide) {
+    if (c->wide || c->det) {
         HIP_TRY(hipMemcpy(c->d_bptr, bptr.data(), sizeof(long long) * bptr.size(), hipMemcpyHostToDevice));
         HIP_TRY(hipMemcpy(c->d_brows, brows.data(), sizeof(unsigned) * brows.size(), hipMemcpyHostToDevice));
     }
@@ -814,6 +869,13 @@ int hmmbw_set_option(hmmbw_ctx *c, int key, int64_t value) {
         HIP_TRY(hipStreamSynchronize(c->stream));
         c->ncopies = (int)value;
         return realloc_stats(c);
+    }
+    if (key == HMMBW_OPT_DETERMINISTIC) {
+        if (c->has_obs) return fail(HMMBW_E_STATE, "set the deterministic mode before hmmbw_set_observations");
+        if (value != 0 && (c->wide || !c->lds_tables()))
+            return fail(HMMBW_E_UNSUPPORTED, "deterministic mode needs N <= 16 and the LDS emission tables");
+        c->det = value != 0;
+        return HMMBW_OK;
     }
     if (key == HMMBW_OPT_MERGE_MSTEP) {
         if (int rc = set_device(c)) return rc;
@@ -862,6 +924,7 @@ int hmmbw_reset_training(hmmbw_ctx *c, double epsilon, int64_t max_iterations) {
     hipLaunchKernelGGL(k_init_state, dim3(1), dim3(1), 0, c->stream, c->state(), epsilon, (long long)max_iterations);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipMemsetAsync(c->d_copies, 0, sizeof(double) * 3 * c->ncopies * c->copy_len(), c->stream));
+    if (c->d_xbuf) HIP_TRY(hipMemsetAsync(c->d_xbuf, 0, sizeof(double) * 3 * (size_t)c->xlen, c->stream));
     c->e_count = 0;
     c->armed = true;
     return HMMBW_OK;
@@ -884,7 +947,7 @@ int hmmbw_estep(hmmbw_ctx *c, double *stats_dev) {
     if (int rc = launch_estep(c, false, c->state(), c->copies(0), llp, nullptr, 0, true)) return rc;
     const long long n = c->copy_len();
     const unsigned grid = (unsigned)std::min<long long>((n + 255) / 256, 64);
-    hipLaunchKernelGGL(k_reduce_local, dim3(grid), dim3(256), 0, c->stream, c->copies(0), c->ncopies, n, llp,
+    hipLaunchKernelGGL(k_reduce_local, dim3(grid), dim3(256), 0, c->stream, c->copies(0), c->det ? 1 : c->ncopies, n, llp,
                        c->nblocks, stats_dev, c->off_ll(), c->world, c->rank, c->state());
     HIP_TRY(hipGetLastError());
     return HMMBW_OK;
@@ -915,15 +978,44 @@ int hmmbw_iterate(hmmbw_ctx *c, int64_t n_iter) {
                                                  "(or use estep / all-reduce / mstep)");
         Rccl *r = nullptr;
         if (int rc = rccl_load(nullptr, &r)) return rc;
+        // small kernels: fused (no k_reduce_local launch); the wide path keeps estep + k_reduce_local
+        const bool fused = !c->wide && c->nwaves > 0 && !c->det;
+        if (fused) {
+            const long long xl = (long long)c->ncopies * c->copy_len() + 2LL * c->world;
+            if (c->xlen != xl) {
+                if (int rc = flush_mstep(c)) return rc;
+                HIP_TRY(hipStreamSynchronize(c->stream));
+                dfree(c->d_xbuf);
+                if (int rc = dalloc(&c->d_xbuf, 3 * (size_t)xl)) return rc;
+                HIP_TRY(hipMemsetAsync(c->d_xbuf, 0, sizeof(double) * 3 * (size_t)xl, c->stream));
+                c->xlen = xl;
+                c->e_count = 0;
+            }
+        }
         for (int64_t i = 0; i < n_iter; ++i) {
-            if (int rc = hmmbw_estep(c, c->d_ext)) return rc;
+            double *ar = c->d_ext;
+            size_t ar_len = (size_t)c->stats_len();
+            if (fused) {
+                if (c->pend.on && !c->can_merge())
+                    if (int rc = flush_mstep(c)) return rc;
+                const long long e = c->e_count++;
+                double *X = c->d_xbuf + (e % 3) * c->xlen, *Xn = c->d_xbuf + ((e + 1) % 3) * c->xlen;
+                const long long ll_off = (long long)c->ncopies * c->copy_len();
+                // accumulate into X (the merged M-step reads the previous, all-reduced X), clear the next
+                if (int rc = launch_estep(c, false, c->state(), X, c->llpart(e), Xn, c->xlen, true,
+                                          X + ll_off + 2LL * c->rank))
+                    return rc;
+                ar = X;
+                ar_len = (size_t)c->xlen;
+            } else if (int rc = hmmbw_estep(c, c->d_ext)) {
+                return rc;
+            }
             hipEvent_t e0 = nullptr, e1 = nullptr;
             if (c->timing && (c->ar_seq++ % c->timing) == 0) {
                 if (int rc = take_events(c->ar_free, &e0, &e1)) return rc;
                 HIP_TRY(hipEventRecord(e0, c->stream));
             }
-            ncclResult_t e = r->all_reduce(c->d_ext, c->d_ext, (size_t)c->stats_len(), ncclFloat64, ncclSum, c->comm,
-                                           c->stream);
+            ncclResult_t e = r->all_reduce(ar, ar, ar_len, ncclFloat64, ncclSum, c->comm, c->stream);
             if (e != ncclSuccess) return rccl_fail(r, e, "ncclAllReduce");
             if (e1) {
                 HIP_TRY(hipEventRecord(e1, c->stream));
@@ -932,7 +1024,21 @@ int hmmbw_iterate(hmmbw_ctx *c, int64_t n_iter) {
                 if (c->ar_pending.size() >= 256)
                     if (int rc = drain_pairs(c->ar_pending, c->ar_free, &c->ar_ms, &c->ar_n)) return rc;
             }
-            if (int rc = hmmbw_mstep(c, c->d_ext, c->R_global)) return rc;
+            if (fused) {
+                hmmbw_ctx::Pending &p = c->pend;
+                p.on = true;
+                p.local = false;
+                p.src = ar;
+                p.nsrc = c->ncopies;
+                p.ll = ar + (long long)c->ncopies * c->copy_len();
+                p.nll = c->world;
+                p.ext = ar;
+                p.R = c->R_global;
+                if (!c->can_merge())
+                    if (int rc = flush_mstep(c)) return rc;
+            } else if (int rc = hmmbw_mstep(c, c->d_ext, c->R_global)) {
+                return rc;
+            }
         }
         return HMMBW_OK;
     }
@@ -949,7 +1055,7 @@ int hmmbw_iterate(hmmbw_ctx *c, int64_t n_iter) {
         p.on = true;
         p.local = true;
         p.src = c->copies(e);
-        p.nsrc = c->ncopies;
+        p.nsrc = c->det ? 1 : c->ncopies;
         p.ll = c->llpart(e);
         p.nll = c->nblocks;
         p.ext = nullptr;

@@ -29,13 +29,20 @@ static __device__ unsigned long long g_phase[kPhaseWaves][8];
         const long long w_ = (long long)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);   \
         if ((threadIdx.x & 63) == 0 && w_ < kPhaseWaves) g_phase[w_][k] = wall_clock64();      \
     } while (0)
-// shader-clock stamp at the start of forward (d = 0) / backward (d = 1) chunk c (c < 64)
+// shader-clock stamp at the start of forward (d = 0) / backward (d = 1) chunk c (c < 64); only with
+// -DHMMBW_CHUNK_TIMES too: its conditional stores inside the sweeps change their s_waitcnt placement
 static __device__ unsigned long long g_chunk[4096][2][64];
+#ifdef HMMBW_CHUNK_TIMES
 #define CHUNKSTAMP(d, c)                                                                       \
     do {                                                                                       \
         const long long w_ = (long long)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);   \
         if ((threadIdx.x & 63) == 0 && w_ < 4096 && (c) < 64) g_chunk[w_][d][c] = clock64();   \
     } while (0)
+#else
+#define CHUNKSTAMP(d, c) \
+    do {                 \
+    } while (0)
+#endif
 #else
 #define CHUNKSTAMP(d, c) \
     do {                 \
@@ -123,6 +130,9 @@ struct EArgs {
     int merged;        // 1: run the previous iteration's M-step (m) in the prologue of every workgroup
     double *zero;      // statistics buffer of the NEXT iteration, cleared by this launch (or nullptr)
     long long zero_len;
+    double *part;      // deterministic mode: per-workgroup partial statistics [blocks][off_bnum]
+    double *rank_ll;   // multi-rank fused: this rank's (max, sum exp) slot in the all-reduce buffer (or nullptr)
+    int *done_ctr;     // ... and the workgroup completion counter that picks the workgroup forming it
     MArgs m;
     long long off_S, off_gex, off_gall, off_bnum;
 };
@@ -327,12 +337,18 @@ __host__ __device__ constexpr size_t lds_table_bytes(int K, int GP) { return (si
 
 template <int N, int G, int GP, bool PT, int BLK = kBlock>
 __device__ bool merged_mstep(const EArgs &a, double *sP, double *sH, double *sPA, long long bid);
+__device__ void rank_ll_pair(const EArgs &a, long long nblk, double *sh);
 
 // Body of the small-N E-step / scorer for workgroup `bid` of the `nblk` workgroups that cover one
 // model's sequences: the whole grid of k_estep_small, or one model's slice of a grouped launch
 // (k_estep_small_group, several models of the same shape in one launch).
-template <int N, int G, bool LR, bool LDSTAB, bool FWD_ONLY>
+// DET (deterministic-reduction mode, LDS tables, E-step only): no floating-point atomics anywhere, so
+// repeated runs are bitwise identical: gamma goes to per-position rows in HBM (summed per symbol in a
+// fixed order by k_bnum_gather, as on the wide path) instead of the LDS histogram, and each workgroup
+// writes its partial statistics with plain stores (summed over workgroups in order by k_det_reduce).
+template <int N, int G, bool LR, bool LDSTAB, bool FWD_ONLY, bool DET = false>
 __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long bid, const long long nblk) {
+    static_assert(!DET || (LDSTAB && !FWD_ONLY), "deterministic mode: E-step with LDS tables");
     constexpr int U = kWave / G;
     constexpr int NS = LR ? 2 : N;      // per-lane S accumulators (row j of S)
     constexpr int NV = NS + 3;          // + gamma_den_excl, gamma_den_all, pi_num
@@ -414,7 +430,8 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
         const int Tw = a.L.wave_T[wave];
         const bool full = a.L.wave_full[wave] != 0;
         const int nch = (Tw + kChunk - 1) / kChunk;
-        const uint16_t *symw = a.L.sym + a.L.wave_symoff[wave] + u * kChunk;
+        const long long symbase = a.L.wave_symoff[wave] + u * kChunk;  // pack index of this slot's chunk-0 entry
+        const uint16_t *symw = a.L.sym + symbase;
         double *ckw = a.ckpt + (FWD_ONLY ? 0 : a.L.wave_ckoff[wave]) + lane;
         uint4 *spw = a.spack + (FWD_ONLY ? 0 : a.L.wave_spoff[wave]) + u;
         const bool jv = j < N;
@@ -767,7 +784,12 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
                     // they are not queued behind them
                     ldrows(bvn, bun, pkn);
 #ifndef HMMBW_NO_HIST  // diagnostics build: no B-numerator histogram
-                    if constexpr (LDSTAB) {
+                    if constexpr (DET) {
+                        // gamma row of every position (position = index of the symbol in the pack layout)
+                        double *gr = a.gam + (symbase + (long long)c * U * kChunk) * G + j;
+#pragma unroll
+                        for (int k = 0; k < kChunk; ++k) gr[k * G] = gk[k];
+                    } else if constexpr (LDSTAB) {
                         // every lane, no branch (the pad lanes j >= N add their zero gamma to the pad
                         // columns), so the compiler's lgkmcnt bookkeeping stays exact
 #pragma unroll
@@ -870,6 +892,9 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
 #pragma unroll
             for (int k = 0; k < NV; ++k) sRed[(wv * G + j) * NV + k] = vals[k];
         }
+        double *sPart = smem;  // DET: this workgroup's statistics [off_bnum] (the tables are dead now)
+        if constexpr (DET)
+            for (long long i = tid; i < a.off_bnum; i += blockDim.x) sPart[i] = 0.0;
         __syncthreads();
         const int nw = blockDim.x >> 6;
         for (int idx = tid; idx < G * NV; idx += blockDim.x) {
@@ -890,9 +915,13 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
             } else {
                 dst = jj;  // pi_num at offset 0
             }
-            unsafeAtomicAdd(&accb[dst], x);
+            if constexpr (DET) sPart[dst] = x;
+            else unsafeAtomicAdd(&accb[dst], x);
         }
-        if constexpr (LDSTAB) {
+        if constexpr (DET) {
+            __syncthreads();
+            for (long long i = tid; i < a.off_bnum; i += blockDim.x) a.part[bid * a.off_bnum + i] = sPart[i];
+        } else if constexpr (LDSTAB) {
             for (int idx = tid; idx < K * G; idx += blockDim.x) {
                 const int k = idx / G, jj = idx - k * G;
                 if (jj >= N) continue;
@@ -902,11 +931,13 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
         }
     }
     PHASE(5);
+    if constexpr (!FWD_ONLY)
+        if (a.rank_ll != nullptr) rank_ll_pair(a, nblk, sRed);
 }
 
-template <int N, int G, bool LR, bool LDSTAB, bool FWD_ONLY>
+template <int N, int G, bool LR, bool LDSTAB, bool FWD_ONLY, bool DET = false>
 __global__ void __launch_bounds__(kBlock, LR ? 2 : 1) k_estep_small(EArgs a) {  // LR: 2 waves per SIMD (<= 256 VGPRs)
-    estep_small_body<N, G, LR, LDSTAB, FWD_ONLY>(a, blockIdx.x, gridDim.x);
+    estep_small_body<N, G, LR, LDSTAB, FWD_ONLY, DET>(a, blockIdx.x, gridDim.x);
 }
 
 // Grouped launch: g.nm models of one shape (same N, topology and tables), model m owning workgroups
@@ -981,6 +1012,29 @@ __device__ void combine_ll_pairs(const double *pairs, long long n, double *sh, d
 
 
 
+// Multi-rank fused E-step (hmmbw_iterate with the engine communicator): the workgroups accumulate
+// straight into the all-reduce buffer, and the LAST workgroup to finish (completion counter) folds the
+// per-workgroup (max, sum exp) pairs into this rank's slot (what k_reduce_local did in its own launch).
+// No __threadfence: a device-scope release writes back the XCD's L2 (this launch's checkpoints), which
+// cost ~20 us per launch; the pairs are memory-side atomics, so thread 0 only has to see its own pair
+// land (vmcnt(0)) before it counts, and the last workgroup reads the pairs with atomics.
+__device__ void rank_ll_pair(const EArgs &a, long long nblk, double *sh) {
+    __shared__ int sLast;
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // s_waitcnt vmcnt(0): block_ll_partial's atomicExch has landed
+        sLast = atomicAdd(a.done_ctr, 1) == (int)(nblk - 1);
+    }
+    __syncthreads();
+    if (!sLast) return;
+    double m, s;
+    combine_ll_pairs<true>(a.llpart, nblk, sh, &m, &s);  // memory-side atomic reads of the pairs
+    if (threadIdx.x == 0) {
+        atomicExch(&a.rank_ll[0], (s > 0.0) ? m : 0.0);
+        atomicExch(&a.rank_ll[1], s);
+        atomicExch(a.done_ctr, 0);
+    }
+}
+
 // sum of one statistic over the copies, clearing them for the next iteration
 template <bool ATOMIC>
 __device__ __forceinline__ double take(const MArgs &m, long long idx) {
@@ -1051,16 +1105,16 @@ __device__ void mstep_block(const MArgs &m) {
         combine_ll_pairs<ATOMIC>(m.llpart, m.nblocks, sh, &mx, &s);
         if (tid == 0) sL = (s > 0.0) ? mx + log(s) : -INFINITY;
     } else if (tid == 0) {
-        const double *ll = m.src + m.off_ll;
+        const double *ll = m.llpart;  // one (max, sum exp) pair per rank, all-reduced
         double mx = -INFINITY;
-        for (int r = 0; r < m.world; ++r)
+        for (long long r = 0; r < m.nblocks; ++r)
             if (ll[2 * r + 1] > 0.0) mx = fmax(mx, ll[2 * r]);
         double s = 0.0;
         if (mx != -INFINITY)
-            for (int r = 0; r < m.world; ++r)
+            for (long long r = 0; r < m.nblocks; ++r)
                 if (ll[2 * r + 1] > 0.0) s += ll[2 * r + 1] * exp(ll[2 * r] - mx);
         sL = (s > 0.0) ? mx + log(s) : -INFINITY;
-        for (int r = 0; r < 2 * m.world; ++r) m.zero_ll[r] = 0.0;
+        for (long long r = 0; r < 2 * m.nblocks; ++r) m.zero_ll[r] = 0.0;
     }
     const int N = m.N, K = m.K;
     for (int i = tid; i < N; i += blockDim.x) {
@@ -1129,13 +1183,13 @@ __device__ void mstep_grid(const MArgs &m) {
         combine_ll_pairs<false>(m.llpart, m.nblocks, sh, &mx, &s);
         if (tid == 0) sL = (s > 0.0) ? mx + log(s) : -INFINITY;
     } else if (tid == 0) {
-        const double *ll = m.src + m.off_ll;
+        const double *ll = m.llpart;  // one (max, sum exp) pair per rank, all-reduced
         double mx = -INFINITY;
-        for (int r = 0; r < m.world; ++r)
+        for (long long r = 0; r < m.nblocks; ++r)
             if (ll[2 * r + 1] > 0.0) mx = fmax(mx, ll[2 * r]);
         double s = 0.0;
         if (mx != -INFINITY)
-            for (int r = 0; r < m.world; ++r)
+            for (long long r = 0; r < m.nblocks; ++r)
                 if (ll[2 * r + 1] > 0.0) s += ll[2 * r + 1] * exp(ll[2 * r] - mx);
         sL = (s > 0.0) ? mx + log(s) : -INFINITY;
     }

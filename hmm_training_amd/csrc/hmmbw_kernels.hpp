@@ -17,6 +17,7 @@ using GroupFn = void (*)(GroupArgs);
 struct Kernels {
     KernelFn estep = nullptr, score = nullptr;
     GroupFn group_estep = nullptr, group_score = nullptr;  // grouped launches (LDS tables only)
+    KernelFn det_estep = nullptr;                          // deterministic-reduction E-step (LDS tables only)
 };
 
 // E-step and scorer kernels for N states (1 <= N <= 16), left-to-right or dense, with or without the
@@ -28,7 +29,7 @@ Kernels small_kernels_n(bool lr, bool ldstab);
 Kernels wide_kernels(int NP);
 
 // The wide path's B-numerator gather (estep_mfma.hpp).
-using BnumFn = void (*)(const double *, const unsigned *, const long long *, int, int, double *, const IterState *);
+using BnumFn = void (*)(const double *, const unsigned *, const long long *, int, int, int, double *, const IterState *);
 BnumFn bnum_gather_kernel();
 
 // The VQ encoder (vq.hip).

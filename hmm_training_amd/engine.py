@@ -16,13 +16,15 @@ otherwise (gloo, or HMMBW_NATIVE_COMM=0) the all-reduce goes through torch.distr
 from __future__ import annotations
 
 import ctypes
+import json
 import os
+import time
 from typing import Callable, List, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
 
-from ._lib import OPT_MERGE_MSTEP, OPT_SAFE_SCALING, OPT_STAT_COPIES, TOPOLOGY, TOPOLOGY_NAME, IterRecord, Status, check, lib
+from ._lib import OPT_DETERMINISTIC, OPT_MERGE_MSTEP, OPT_SAFE_SCALING, OPT_STAT_COPIES, TOPOLOGY, TOPOLOGY_NAME, IterRecord, Status, check, lib
 
 IterCallback = Callable[[int, float, float], None]
 
@@ -109,7 +111,8 @@ class BaumWelchEngine:
 
     def __init__(self, n_states: int, n_symbols: int, device: Optional[int] = None, topology: str = "auto",
                  rank: int = 0, world_size: int = 1, stream: Optional[int] = None, safe_scaling: bool = False,
-                 merge_mstep: bool = True, stat_copies: Optional[int] = None, group=None, native_comm: Optional[bool] = None):
+                 merge_mstep: bool = True, stat_copies: Optional[int] = None, group=None, native_comm: Optional[bool] = None,
+                 deterministic: bool = False):
         self._lib = lib()
         self.N, self.M = int(n_states), int(n_symbols)
         self.device = default_device() if device is None else int(device)
@@ -130,6 +133,8 @@ class BaumWelchEngine:
             check(self._lib.hmmbw_set_option(self._ctx, OPT_MERGE_MSTEP, 0))
         if stat_copies is not None:  # None: the library default (2)
             check(self._lib.hmmbw_set_option(self._ctx, OPT_STAT_COPIES, int(stat_copies)))
+        if deterministic:  # bitwise-reproducible statistics (no fp atomics); before set_observations
+            check(self._lib.hmmbw_set_option(self._ctx, OPT_DETERMINISTIC, 1))
         self.n_seq = 0
         self.n_seq_global = 0
         self._group = group
@@ -149,6 +154,7 @@ class BaumWelchEngine:
         R = len(offsets) - 1
         check(self._lib.hmmbw_set_observations(self._ctx, offsets.ctypes.data, symbols.ctypes.data, R))
         self.n_seq = R
+        self.n_symbols_total = int(offsets[-1]) if R > 0 else 0
         self.n_seq_global = R if n_seq_global is None else int(n_seq_global)
         if self._want_native and self._native_R != self.n_seq_global:
             self._native = self._init_native_comm()
@@ -233,27 +239,66 @@ class BaumWelchEngine:
         return torch.zeros(self.stats_len, dtype=torch.float64, device=f"cuda:{self.device}")
 
     def train(self, epsilon: float = 1e-6, max_iterations: int = 100, on_iteration: Optional[IterCallback] = None,
-              group=None, max_chunk: int = 32) -> Status:
-        """Run EM to the reference's stop rule; on_iteration(k, L_k, diff_k) for every iteration."""
+              group=None, max_chunk: int = 32, metrics: Optional[str] = None) -> Status:
+        """Run EM to the reference's stop rule; on_iteration(k, L_k, diff_k) for every iteration.
+
+        metrics (or the HMMBW_METRICS environment variable): a JSONL file that rank 0 appends one line
+        per EM iteration to (see _write_metrics)."""
         self.reset(epsilon, max_iterations)
         stats = self.make_stats_buffer() if self.world_size > 1 and not self._native else None
+        mpath = metrics if metrics is not None else os.environ.get("HMMBW_METRICS")
+        mfh = open(mpath, "a") if (mpath and self.rank == 0) else None
+        if mfh is not None:
+            self.timing(1)
+            self.comm_info(reset=True)
         reported, chunk = 0, 1
-        while True:
-            st, _ = self.status()
-            if st.done:
-                break
-            n = max(1, min(chunk, int(max_iterations) - st.iterations))
-            self.enqueue_iterations(n, stats, group)
-            st, recs = self.status(reported, 0)
-            if on_iteration is not None and st.iterations > reported:
-                st, recs = self.status(reported, st.iterations - reported)
-                for k, (L, d) in enumerate(recs):
-                    on_iteration(reported + k, L, d)
-            reported = st.iterations
-            chunk = min(chunk * 2, max_chunk)
-            if st.done:
-                break
+        try:
+            while True:
+                st, _ = self.status()
+                if st.done:
+                    break
+                n = max(1, min(chunk, int(max_iterations) - st.iterations))
+                t0 = time.perf_counter()
+                self.enqueue_iterations(n, stats, group)
+                st, recs = self.status(reported, 0)
+                wall = time.perf_counter() - t0
+                new = st.iterations - reported
+                recs = self.status(reported, new)[1] if new > 0 and (on_iteration is not None or mfh) else []
+                if on_iteration is not None:
+                    for k, (L, d) in enumerate(recs):
+                        on_iteration(reported + k, L, d)
+                if mfh is not None and new > 0:
+                    self._write_metrics(mfh, reported, recs, wall, n)
+                reported = st.iterations
+                chunk = min(chunk * 2, max_chunk)
+                if st.done:
+                    break
+        finally:
+            if mfh is not None:
+                self.timing(0)
+                mfh.close()
         return st
+
+    def _write_metrics(self, fh, first: int, recs, wall_s: float, enqueued: int) -> None:
+        """One JSON line per iteration of the chunk: L and diff (hmm_training.py:503-514), the chunk's
+        wall time per enqueued iteration (incl. the host status sync), utterances/s/iter over all ranks,
+        the mean E-step kernel time (HIP events), the SURVEY §8(d) byte model over it as GB/s and as a
+        fraction of the 8 TB/s HBM peak, and the mean RCCL all-reduce time (engine communicator)."""
+        k_ms, k_n = self.timing(1)
+        _, ar_ms, ar_n = self.comm_info(reset=True)
+        estep_s = k_ms / k_n / 1e3 if k_n else None
+        nbytes = 24 * self.n_symbols_total + 16 * self.N * self.n_symbols_total + 8 * self.n_seq
+        per_iter = wall_s / max(enqueued, 1)
+        for k, (L, d) in enumerate(recs):
+            row = {"iteration": first + k + 1, "log_likelihood": L, "diff": d if d != float("inf") else None,
+                   "ms_per_iter": 1e3 * per_iter, "utt_per_s_iter": self.n_seq_global / per_iter,
+                   "estep_us": 1e6 * estep_s if estep_s else None,
+                   "hbm_model_gbs": nbytes / estep_s / 1e9 if estep_s else None,
+                   "roofline_frac": nbytes / estep_s / 8e12 if estep_s else None,
+                   "allreduce_us": 1e3 * ar_ms / ar_n if ar_n else None,
+                   "ranks": self.world_size, "sequences_global": self.n_seq_global}
+            fh.write(json.dumps(row) + "\n")
+        fh.flush()
 
     # -------------------------------------------------------------------------------- results
     def params(self, normalise: bool = True) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:

@@ -161,6 +161,12 @@ int hmmbw_score(hmmbw_ctx *ctx, double *out);
  * each workgroup straight into its LDS tables (when the emission tables fit LDS); 0: a separate
  * one-workgroup M-step kernel after every E-step. */
 #define HMMBW_OPT_MERGE_MSTEP 4
+/* 1: deterministic-reduction mode, bitwise-identical results run to run (no floating-point atomics):
+ * gamma goes to per-position rows summed per symbol in a fixed order, and the other statistics are
+ * per-workgroup partials summed in workgroup order.  About twice the E-step time.  Small state counts
+ * (N <= 16) with the LDS emission tables only (HMMBW_E_UNSUPPORTED otherwise); set it before
+ * hmmbw_set_observations (HMMBW_E_STATE after).  Default 0. */
+#define HMMBW_OPT_DETERMINISTIC 7
 int hmmbw_set_option(hmmbw_ctx *ctx, int key, int64_t value);
 
 /* E-step kernel timing with HIP events on the context stream (for bench/roofline).  Returns the

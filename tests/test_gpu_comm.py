@@ -24,30 +24,39 @@ def rccl_path():
     return p.encode() if os.path.exists(p) else None
 
 
-@pytest.mark.parametrize("topology,maxit", [("left_to_right", 8), ("dense", 5)])
-def test_native_comm_one_rank_matches_oracle(oracle, topology, maxit):
+@pytest.mark.parametrize("topology,maxit,N,K,eps,copies", [
+    ("left_to_right", 8, 8, 256, 1e-6, None),   # fused path: E-step into the all-reduce buffer
+    ("dense", 5, 8, 256, 1e-6, None),
+    ("left_to_right", 40, 5, 64, 1e-3, 1),      # converges before maxit (device-side stop rule)
+    ("dense", 4, 8, 256, 1e-6, 3),
+    ("dense", 3, 40, 96, 1e-6, None),           # wide path: estep + k_reduce_local + all-reduce
+])
+def test_native_comm_one_rank_matches_oracle(oracle, topology, maxit, N, K, eps, copies):
     from hmm_training_amd._lib import check, lib
     from hmm_training_amd.engine import BaumWelchEngine
     from hmm_training_amd.hmm_training import default_initial_params
     rng = np.random.default_rng(17)
-    N, K, R = 8, 256, 600
+    R = 600
     obs = [rng.integers(0, K, size=int(t)) for t in rng.integers(40, 220, size=R)]
     pi, A, B = default_initial_params(N, K)
     if topology == "dense":
         A = 0.5 * A + 0.5 * rng.dirichlet(np.ones(N), size=N)
     L = lib()
-    with BaumWelchEngine(N, K, device=0) as e:
+    with BaumWelchEngine(N, K, device=0, stat_copies=copies) as e:
         check(L.hmmbw_set_rank(e._ctx, 0, 1))
         e.set_observations(obs)
         e.set_params(pi, A, B)
         uid = ctypes.create_string_buffer(128)
         check(L.hmmbw_comm_unique_id(rccl_path(), uid))
         check(L.hmmbw_comm_init(e._ctx, rccl_path(), uid, 0, 1, R))
+        e.timing(1)
         trace = []
-        st = e.train(1e-6, maxit, lambda k, Lk, d: trace.append(Lk))
+        st = e.train(eps, maxit, lambda k, Lk, d: trace.append(Lk))
         p2, A2, B2 = e.params()
+        ranks, ar_ms, ar_n = e.comm_info()
+        assert ranks == 1 and ar_n >= st.iterations and ar_ms > 0  # chunks past convergence still all-reduce
     off = np.concatenate([[0], np.cumsum([len(o) for o in obs])]).astype(np.int64)
-    ref = oracle.hmm_training(off, np.concatenate(obs).astype(np.int64), N, K, 1e-6, maxit, pi, A, B)
+    ref = oracle.hmm_training(off, np.concatenate(obs).astype(np.int64), N, K, eps, maxit, pi, A, B)
     assert st.iterations == ref.iterations
     np.testing.assert_allclose(trace, ref.trace_L, rtol=1e-9)
     for mine, theirs in ((A2, ref.A), (B2, ref.B), (p2, ref.pi)):

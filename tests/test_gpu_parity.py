@@ -417,3 +417,22 @@ def test_dropin_two_processes_gloo(case, tmp_path):
             assert lines == list(d["stdout"])
         else:
             assert lines == [], "only rank 0 prints the reference's progress lines"
+
+
+def test_metrics_jsonl_stream(tmp_path):
+    """§5 metrics: BaumWelchEngine.train(metrics=...) appends one JSON line per EM iteration with L,
+    diff, ms/iter, utt/s/iter, E-step kernel time and the byte-model roofline fraction."""
+    import json
+    from hmm_training_amd.engine import BaumWelchEngine
+    d = load("converge")
+    N, M = int(d["N"]), int(d["M"])
+    path = tmp_path / "m.jsonl"
+    with BaumWelchEngine(N, M) as eng:
+        eng.set_observations(observations(d))
+        eng.set_params(d["init_pi"], d["init_A"], d["init_B"])
+        st = eng.train(float(d["epsilon"]), int(d["max_iterations"]), metrics=str(path))
+    rows = [json.loads(l) for l in path.read_text().splitlines()]
+    assert [r["iteration"] for r in rows] == list(range(1, st.iterations + 1))
+    assert_ll([r["log_likelihood"] for r in rows], d["trace_L"])
+    assert rows[0]["diff"] is None and all(r["estep_us"] > 0 and r["utt_per_s_iter"] > 0 for r in rows)
+    assert all(0 < r["roofline_frac"] for r in rows)

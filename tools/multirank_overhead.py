@@ -18,6 +18,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--R", type=int, default=10000)
+    ap.add_argument("--modes", default="single,multirank,native")
     a = ap.parse_args()
     import torch
     import torch.distributed as dist
@@ -33,7 +34,7 @@ def main():
     off = np.arange(R + 1, dtype=np.int64) * T
     pi, A, B = default_initial_params(N, K)
     out = {}
-    for mode in ("single", "multirank", "native"):
+    for mode in a.modes.split(","):
         eng = BaumWelchEngine(N, K, device=0, rank=0, world_size=1)
         eng.set_observations(offsets=off, symbols=sym)
         eng.set_params(pi, A, B)
