@@ -210,8 +210,12 @@ def cpu_baseline(N, K, T, topology, budget_s, seed, symbols="U", threads=0):
     try:
         probe_R = 8 * nth
         dt = run(probe_R)
-        R = int(max(probe_R, min(400_000, probe_R * budget_s / max(dt, 1e-6))))
-        dt = run(R)
+        # batches of at most 200,000 sequences (bounded host memory) until the time budget is spent
+        batch = int(max(probe_R, min(200_000, probe_R * budget_s / max(dt, 1e-6))))
+        R, dt = 0, 0.0
+        while dt < budget_s and R < 5_000_000:
+            dt += run(batch)
+            R += batch
     finally:
         O.set_threads(1)
     value = R / dt
