@@ -979,9 +979,13 @@ int hmmbw_iterate(hmmbw_ctx *c, int64_t n_iter) {
         Rccl *r = nullptr;
         if (int rc = rccl_load(nullptr, &r)) return rc;
         // small kernels: fused (no k_reduce_local launch); the wide path keeps estep + k_reduce_local
-        const bool fused = !c->wide && c->nwaves > 0 && !c->det;
+        // (rank-independent: every rank must all-reduce the same buffer layout, also a rank whose
+        // shard is empty)
+        const bool fused = !c->wide && !c->det;
         if (fused) {
-            const long long xl = (long long)c->ncopies * c->copy_len() + 2LL * c->world;
+            // rounded to 256 B so all three buffers keep the copies' alignment (a 16-B shift splits the
+            // B-numerator rows' 64-B segments over two cache lines; ~0.7 us per launch at cfg3)
+            const long long xl = ((long long)c->ncopies * c->copy_len() + 2LL * c->world + 31) / 32 * 32;
             if (c->xlen != xl) {
                 if (int rc = flush_mstep(c)) return rc;
                 HIP_TRY(hipStreamSynchronize(c->stream));
@@ -1002,9 +1006,13 @@ int hmmbw_iterate(hmmbw_ctx *c, int64_t n_iter) {
                 double *X = c->d_xbuf + (e % 3) * c->xlen, *Xn = c->d_xbuf + ((e + 1) % 3) * c->xlen;
                 const long long ll_off = (long long)c->ncopies * c->copy_len();
                 // accumulate into X (the merged M-step reads the previous, all-reduced X), clear the next
-                if (int rc = launch_estep(c, false, c->state(), X, c->llpart(e), Xn, c->xlen, true,
-                                          X + ll_off + 2LL * c->rank))
-                    return rc;
+                if (c->nblocks > 0) {
+                    if (int rc = launch_estep(c, false, c->state(), X, c->llpart(e), Xn, c->xlen, true,
+                                              X + ll_off + 2LL * c->rank))
+                        return rc;
+                } else {  // empty shard: contribute zeros (no E-step launch clears the buffers)
+                    HIP_TRY(hipMemsetAsync(X, 0, sizeof(double) * (size_t)c->xlen, c->stream));
+                }
                 ar = X;
                 ar_len = (size_t)c->xlen;
             } else if (int rc = hmmbw_estep(c, c->d_ext)) {
@@ -1015,8 +1023,10 @@ int hmmbw_iterate(hmmbw_ctx *c, int64_t n_iter) {
                 if (int rc = take_events(c->ar_free, &e0, &e1)) return rc;
                 HIP_TRY(hipEventRecord(e0, c->stream));
             }
-            ncclResult_t e = r->all_reduce(ar, ar, ar_len, ncclFloat64, ncclSum, c->comm, c->stream);
-            if (e != ncclSuccess) return rccl_fail(r, e, "ncclAllReduce");
+            if (c->world > 1) {  // a 1-rank sum is the identity: RCCL would still launch copy kernels
+                ncclResult_t e = r->all_reduce(ar, ar, ar_len, ncclFloat64, ncclSum, c->comm, c->stream);
+                if (e != ncclSuccess) return rccl_fail(r, e, "ncclAllReduce");
+            }
             if (e1) {
                 HIP_TRY(hipEventRecord(e1, c->stream));
                 c->ar_pending.push_back(e0);

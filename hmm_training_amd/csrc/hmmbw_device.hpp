@@ -337,7 +337,8 @@ __host__ __device__ constexpr size_t lds_table_bytes(int K, int GP) { return (si
 
 template <int N, int G, int GP, bool PT, int BLK = kBlock>
 __device__ bool merged_mstep(const EArgs &a, double *sP, double *sH, double *sPA, long long bid);
-__device__ void rank_ll_pair(const EArgs &a, long long nblk, double *sh);
+__device__ int rank_ll_count(const EArgs &a);
+__device__ void rank_ll_fold(const EArgs &a, long long nblk);
 
 // Body of the small-N E-step / scorer for workgroup `bid` of the `nblk` workgroups that cover one
 // model's sequences: the whole grid of k_estep_small, or one model's slice of a grouped launch
@@ -872,6 +873,11 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
     __syncthreads();
     block_ll_partial(logp_lane, ll_valid, sRed, a.llpart + 2 * bid);
     PHASE(4);
+    // fused multi-rank launch: thread 0 counts this workgroup's pair in during the statistics flush (the
+    // ticket's round trip overlaps the flush), and wave 0 of the last one folds the pairs at the end
+    const bool fused_ll = !FWD_ONLY && !DET && a.rank_ll != nullptr;
+    int ticket = 0;
+    bool counted = false;
 
     if constexpr (!FWD_ONLY) if (!(a.ablate & 1)) {
         // ---- reduce per-lane accumulators over the U sequences of the wave, then the block ----
@@ -896,6 +902,8 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
         if constexpr (DET)
             for (long long i = tid; i < a.off_bnum; i += blockDim.x) sPart[i] = 0.0;
         __syncthreads();
+        if (fused_ll && tid == 0) ticket = rank_ll_count(a);
+        counted = true;
         const int nw = blockDim.x >> 6;
         for (int idx = tid; idx < G * NV; idx += blockDim.x) {
             const int jj = idx / NV, k = idx % NV;
@@ -931,8 +939,10 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
         }
     }
     PHASE(5);
-    if constexpr (!FWD_ONLY)
-        if (a.rank_ll != nullptr) rank_ll_pair(a, nblk, sRed);
+    if (fused_ll && wv == 0) {
+        if (!counted && tid == 0) ticket = rank_ll_count(a);
+        if (__shfl(ticket, 0) == (int)(nblk - 1)) rank_ll_fold(a, nblk);
+    }
 }
 
 template <int N, int G, bool LR, bool LDSTAB, bool FWD_ONLY, bool DET = false>
@@ -1011,29 +1021,6 @@ __device__ void combine_ll_pairs(const double *pairs, long long n, double *sh, d
 }
 
 
-
-// Multi-rank fused E-step (hmmbw_iterate with the engine communicator): the workgroups accumulate
-// straight into the all-reduce buffer, and the LAST workgroup to finish (completion counter) folds the
-// per-workgroup (max, sum exp) pairs into this rank's slot (what k_reduce_local did in its own launch).
-// No __threadfence: a device-scope release writes back the XCD's L2 (this launch's checkpoints), which
-// cost ~20 us per launch; the pairs are memory-side atomics, so thread 0 only has to see its own pair
-// land (vmcnt(0)) before it counts, and the last workgroup reads the pairs with atomics.
-__device__ void rank_ll_pair(const EArgs &a, long long nblk, double *sh) {
-    __shared__ int sLast;
-    if (threadIdx.x == 0) {
-        __builtin_amdgcn_s_waitcnt(0x0F70);  // s_waitcnt vmcnt(0): block_ll_partial's atomicExch has landed
-        sLast = atomicAdd(a.done_ctr, 1) == (int)(nblk - 1);
-    }
-    __syncthreads();
-    if (!sLast) return;
-    double m, s;
-    combine_ll_pairs<true>(a.llpart, nblk, sh, &m, &s);  // memory-side atomic reads of the pairs
-    if (threadIdx.x == 0) {
-        atomicExch(&a.rank_ll[0], (s > 0.0) ? m : 0.0);
-        atomicExch(&a.rank_ll[1], s);
-        atomicExch(a.done_ctr, 0);
-    }
-}
 
 // sum of one statistic over the copies, clearing them for the next iteration
 template <bool ATOMIC>
@@ -1314,6 +1301,48 @@ __device__ __forceinline__ double wave_max(double x) {
     x = fmax(x, dpp<0x140>(x));
     x = fmax(x, __shfl_xor(x, 16));
     return fmax(x, __shfl_xor(x, 32));
+}
+
+// Multi-rank fused E-step (hmmbw_iterate with the engine communicator): the workgroups accumulate
+// straight into the all-reduce buffer, and wave 0 of the LAST workgroup to count its pair in (completion
+// counter) folds the per-workgroup (max, sum exp) pairs into this rank's slot (what k_reduce_local did
+// in its own launch).  No __threadfence: a device-scope release writes back the XCD's L2 (this launch's
+// checkpoints), which cost ~20 us per launch; the pairs are memory-side atomics, so thread 0 only has
+// to see its own pair land (vmcnt(0)) before it counts, and the folding wave reads them with atomics.
+__device__ int rank_ll_count(const EArgs &a) {
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // s_waitcnt vmcnt(0): block_ll_partial's atomicExch has landed
+    return atomicAdd(a.done_ctr, 1);
+}
+
+__device__ void rank_ll_fold(const EArgs &a, long long nblk) {  // one wave
+    const int lane = threadIdx.x & 63;
+    double tm = -INFINITY, ts = 0.0;
+    for (long long r0 = 0; r0 < nblk; r0 += 4 * 64) {
+        double pm[4], ps[4];  // every round's memory-side reads issued together
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const long long r = r0 + lane + q * 64;
+            pm[q] = r < nblk ? rd<true>(&a.llpart[2 * r]) : 0.0;
+            ps[q] = r < nblk ? rd<true>(&a.llpart[2 * r + 1]) : 0.0;
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            if (!(ps[q] > 0.0)) continue;
+            if (pm[q] > tm) {
+                ts = (tm == -INFINITY) ? ps[q] : ps[q] + ts * exp(tm - pm[q]);
+                tm = pm[q];
+            } else {
+                ts += ps[q] * exp(pm[q] - tm);
+            }
+        }
+    }
+    const double mx = wave_max(tm);
+    const double s = gsum<64>((mx != -INFINITY && ts > 0.0) ? ts * exp(tm - mx) : 0.0);
+    if (lane == 0) {
+        atomicExch(&a.rank_ll[0], (s > 0.0) ? mx : 0.0);
+        atomicExch(&a.rank_ll[1], s);
+        atomicExch(a.done_ctr, 0);
+    }
 }
 
 template <int N, int G, int GP, bool PT, int BLK>
