@@ -131,11 +131,15 @@ __global__ void __launch_bounds__(NT * 64, 2) k_estep_mfma(EArgs a) {  // 2 wave
     // b(o_t) in slot t % 4, loaded kLook steps ahead; symbol packs one chunk ahead of their use
     constexpr int kLook = 3;
     f64x4 bring[4];
-    auto fstep = [&](int t, const f64x4 &b, auto MASK_) HMMBW_AI {
+    // STEADY: a step of a chunk in which every step runs (t >= 1): no branch in the step, so the
+    // compiler can count the in-flight prefetches and stores (a conditional block makes it wait for
+    // them: gfx9 counts stores in vmcnt)
+    auto fstep = [&](int t, const f64x4 &b, auto MASK_, auto STEADY_) HMMBW_AI {
         constexpr bool MASK = decltype(MASK_)::value;
+        constexpr bool STEADY = decltype(STEADY_)::value;
         f64x4 x;
         int sc = 0;
-        if (t == 0) {
+        if (!STEADY && t == 0) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int j = 16 * m + g + 4 * r;
@@ -146,12 +150,11 @@ __global__ void __launch_bounds__(NT * 64, 2) k_estep_mfma(EArgs a) {  // 2 wave
             double zb[KB];
 #pragma unroll
             for (int kb = 0; kb < KB; ++kb) zb[kb] = src[4 * kb * kXs];
-            f64x4 acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
+            // one accumulation chain: a dependent v_mfma_f64_16x16x4 issues every 64 cycles, its full
+            // rate (tools/ubench_mfma.hip), and a second chain would cost 8 VGPRs
+            f64x4 acc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-            for (int kb = 0; kb < KB; kb += 2) {
-                acc0 = mfma_f64(aop[kb], zb[kb], acc0);
-                acc1 = mfma_f64(aop[kb + 1], zb[kb + 1], acc1);
-            }
+            for (int kb = 0; kb < KB; ++kb) acc = mfma_f64(aop[kb], zb[kb], acc);
             // s_t from z_{t-1} over all NP states of the sequence (4 lanes x KB values)
             int M = 0;
 #pragma unroll
@@ -161,7 +164,7 @@ __global__ void __launch_bounds__(NT * 64, 2) k_estep_mfma(EArgs a) {  // 2 wave
             sc = M == 0 ? 0 : M - 1023;
             // rescale before the emission factor: z_{t-1} and b(o_t) may both be ~1e-200 (no underflow)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) x[r] = __builtin_amdgcn_ldexp(acc0[r] + acc1[r], -sc) * b[r];
+            for (int r = 0; r < 4; ++r) x[r] = __builtin_amdgcn_ldexp(acc[r], -sc) * b[r];
         }
         if constexpr (MASK) {
             const bool act = t < T;  // past the sequence's end: z frozen at z_{T-1}
@@ -178,27 +181,36 @@ __global__ void __launch_bounds__(NT * 64, 2) k_estep_mfma(EArgs a) {  // 2 wave
 #pragma unroll
                 for (int r = 0; r < 4; ++r) ckw[((long long)t * NT * 4 + r) * 64] = z[r];
             }
-            if (m == 0 && g == 0) ew[t * kTileSeqs] = sc;
+            // every wave computes the same s_t from all NP states: one lane group stores it (STEADY: all
+            // lanes, the same value to the same 16 words, so the store needs no exec branch)
+            if (STEADY || (m == 0 && g == 0)) ew[t * kTileSeqs] = sc;
         }
         if (!WIDE_ABL(a, 16)) __syncthreads();
     };
+    uint4 p0, p1;  // symbol packs of chunks c and c + 1
+    auto fchunk = [&](int c, auto MASK_, auto STEADY_) HMMBW_AI {
+        constexpr bool STEADY = decltype(STEADY_)::value;
+        const uint4 p2 = loadpack(c + 2 < nch ? c + 2 : nch - 1);
+#pragma unroll
+        for (int k = 0; k < kChunk; ++k) {
+            const int t = c * kChunk + k;
+            // b(o_{t + kLook}) into the slot step t - 1 has consumed
+            bring[(k + kLook) & 3] = emis(k + kLook < kChunk ? sym_of(p0, k + kLook) : sym_of(p1, k + kLook - kChunk));
+            if (!STEADY && t >= Tw) continue;  // tile-uniform
+            fstep(t, bring[k & 3], MASK_, STEADY_);
+        }
+        p0 = p1;
+        p1 = p2;
+    };
     auto forward = [&](auto MASK_) HMMBW_AI {
-        uint4 p0 = loadpack(0), p1 = loadpack(nch > 1 ? 1 : 0);  // chunks c and c + 1
+        p0 = loadpack(0);
+        p1 = loadpack(nch > 1 ? 1 : 0);
 #pragma unroll
         for (int i = 0; i < kLook; ++i) bring[i] = emis(sym_of(p0, i));
-        for (int c = 0; c < nch; ++c) {
-            const uint4 p2 = loadpack(c + 2 < nch ? c + 2 : nch - 1);
-#pragma unroll
-            for (int k = 0; k < kChunk; ++k) {
-                const int t = c * kChunk + k;
-                // b(o_{t + kLook}) into the slot step t - 1 has consumed
-                bring[(k + kLook) & 3] = emis(k + kLook < kChunk ? sym_of(p0, k + kLook) : sym_of(p1, k + kLook - kChunk));
-                if (t >= Tw) continue;  // tile-uniform
-                fstep(t, bring[k & 3], MASK_);
-            }
-            p0 = p1;
-            p1 = p2;
-        }
+        const int cf = Tw / kChunk;  // chunks [1, cf) run all their steps
+        fchunk(0, MASK_, std::false_type{});
+        for (int c = 1; c < cf; ++c) fchunk(c, MASK_, std::true_type{});
+        for (int c = cf > 1 ? cf : 1; c < nch; ++c) fchunk(c, MASK_, std::false_type{});
     };
     if (full) forward(std::false_type{});
     else forward(std::true_type{});
@@ -248,9 +260,9 @@ __global__ void __launch_bounds__(NT * 64, 2) k_estep_mfma(EArgs a) {  // 2 wave
         f64x4 S[NT];
 #pragma unroll
         for (int mm = 0; mm < NT; ++mm) S[mm] = f64x4{0.0, 0.0, 0.0, 0.0};
-        // rings: alpha_hat_t (HBM) in slot t % 4, loaded kLook steps ahead; b(o_{t+1}) (L2-resident
+        // rings: alpha_hat_t (HBM) in slot t % 2, loaded two steps ahead; b(o_{t+1}) (L2-resident
         // table) and s_{t+1} in slot t % 2, loaded one step ahead (fewer VGPRs: two waves per SIMD)
-        f64x4 zring[4], bring1[2];
+        f64x4 zring[2], bring1[2];
         int sring[2];
         auto ldz = [&](int t) HMMBW_AI -> f64x4 {
             f64x4 v;
@@ -260,8 +272,9 @@ __global__ void __launch_bounds__(NT * 64, 2) k_estep_mfma(EArgs a) {  // 2 wave
             return v;
         };
         // one regular step t <= Tw - 2 (MASK: per-sequence t <= T - 2 in ragged tiles)
-        auto bstep = [&](int t, const f64x4 &zt, const f64x4 &b1, int s1, auto MASK_) HMMBW_AI {
+        auto bstep = [&](int t, const f64x4 &zt, const f64x4 &b1, int s1, auto MASK_, auto STEADY_) HMMBW_AI {
             constexpr bool MASK = decltype(MASK_)::value;
+            constexpr bool STEADY = decltype(STEADY_)::value;
             const bool reg = !MASK || t <= T - 2;
             f64x4 v, zs;
 #pragma unroll
@@ -281,12 +294,9 @@ __global__ void __launch_bounds__(NT * 64, 2) k_estep_mfma(EArgs a) {  // 2 wave
             if (!WIDE_ABL(a, 16)) __syncthreads();
             // beta_hat_t = A v (:163-199), this wave's 16 rows
             const double *vsrc = bopb + p * IMG;
-            f64x4 acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
+            f64x4 acc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-            for (int kb = 0; kb < KB; kb += 2) {
-                acc0 = mfma_f64(aop[kb], vsrc[4 * kb * kXs], acc0);
-                acc1 = mfma_f64(aop[kb + 1], vsrc[4 * (kb + 1) * kXs], acc1);
-            }
+            for (int kb = 0; kb < KB; ++kb) acc = mfma_f64(aop[kb], vsrc[4 * kb * kXs], acc);
             // S_ij += sum_s z_t(i, s) v_{t+1}(j, s): xi_t(i,j) / a_ij (:396-410)
             const double *tsrc = topb + p * IMG;
 #pragma unroll
@@ -298,14 +308,14 @@ __global__ void __launch_bounds__(NT * 64, 2) k_estep_mfma(EArgs a) {  // 2 wave
             f64x4 gm;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const double bn = acc0[r] + acc1[r];
+                const double bn = acc[r];
                 gm[r] = zs[r] * bn;  // gamma_t (:392); 0 past the sequence's end
                 if constexpr (MASK) beta[r] = reg ? bn : beta[r];
                 else beta[r] = bn;
                 gex[r] += gm[r];
             }
             if ((!MASK || reg) && !WIDE_ABL(a, 4)) putg(t, gm);  // B numerator row (:474-485)
-            if (t == 0) {  // pi_num (:415-420): gamma_0 summed over the tile's sequences
+            if (!STEADY && t == 0) {  // pi_num (:415-420): gamma_0 summed over the tile's sequences
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int j = 16 * m + g + 4 * r;
@@ -314,35 +324,44 @@ __global__ void __launch_bounds__(NT * 64, 2) k_estep_mfma(EArgs a) {  // 2 wave
                 }
             }
         };
+        uint4 pc;  // chunk c's symbol pack; chunk c - 1's is loaded at the top of chunk c
+        auto bchunk = [&](int c, auto MASK_, auto STEADY_) HMMBW_AI {
+            constexpr bool STEADY = decltype(STEADY_)::value;  // c >= 1 and every step t <= Tw - 2
+            const uint4 pp = loadpack(c >= 1 ? c - 1 : 0);
+#pragma unroll
+            for (int k = kChunk - 1; k >= 0; --k) {
+                const int t = c * kChunk + k;
+                // b(o_t), s_t and alpha_hat_{t - kLook} into the slots step t + 1 has consumed; the
+                // one-step-ahead loads go first so that waiting for them (in-order vmcnt) leaves
+                // the deeper alpha_hat prefetch in flight
+                if (STEADY || t >= 1) {
+                    bring1[(k + 1) & 1] = emis(sym_of(pc, k));  // b(o_t), consumed by step t - 1
+                    sring[(k + 1) & 1] = ew[t * kTileSeqs];     // s_t
+                }
+                // tile-uniform; gamma_{T-1} is done above
+                if (STEADY || t <= Tw - 2) bstep(t, zring[k & 1], bring1[k & 1], sring[k & 1], MASK_, STEADY_);
+                // alpha_hat_{t-2} into the slot step t has just consumed (two in flight: VGPR budget)
+                if (STEADY || t >= 2) zring[k & 1] = ldz(t - 2);
+            }
+            pc = pp;
+        };
         auto backward = [&](auto MASK_) HMMBW_AI {
             const int ttop = nch * kChunk;  // steps ttop - 1 .. 0 are visited (those > Tw - 2 skip)
-            uint4 pc = loadpack(nch - 1);   // chunk c; chunk c - 1's pack is loaded at the top of chunk c
-            // alpha_hat of the first kLook visited steps s = ttop - 1 - i; step ttop - 1 has no o_{s+1}
+            pc = loadpack(nch - 1);
+            // alpha_hat of the first two visited steps s = ttop - 1 - i; step ttop - 1 has no o_{s+1}
 #pragma unroll
-            for (int i = 0; i < kLook; ++i) {
+            for (int i = 0; i < 2; ++i) {
                 const int s0 = ttop - 1 - i;
-                zring[s0 & 3] = s0 >= 0 ? ldz(s0) : f64x4{0.0, 0.0, 0.0, 0.0};
+                zring[s0 & 1] = s0 >= 0 ? ldz(s0) : f64x4{0.0, 0.0, 0.0, 0.0};
             }
             bring1[1] = f64x4{0.0, 0.0, 0.0, 0.0};
             sring[1] = 0;
-            for (int c = nch - 1; c >= 0; --c) {
-                const uint4 pp = loadpack(c >= 1 ? c - 1 : 0);
-#pragma unroll
-                for (int k = kChunk - 1; k >= 0; --k) {
-                    const int t = c * kChunk + k;
-                    // b(o_t), s_t and alpha_hat_{t - kLook} into the slots step t + 1 has consumed; the
-                    // one-step-ahead loads go first so that waiting for them (in-order vmcnt) leaves
-                    // the deeper alpha_hat prefetch in flight
-                    if (t >= 1) {
-                        bring1[(k + 1) & 1] = emis(sym_of(pc, k));  // b(o_t), consumed by step t - 1
-                        sring[(k + 1) & 1] = ew[t * kTileSeqs];     // s_t
-                    }
-                    if (t - kLook >= 0) zring[(k - kLook) & 3] = ldz(t - kLook);
-                    if (t > Tw - 2) continue;  // tile-uniform; gamma_{T-1} is done above
-                    bstep(t, zring[k & 3], bring1[k & 1], sring[k & 1], MASK_);
-                }
-                pc = pp;
-            }
+            // chunks [1, cs] have every step t <= Tw - 2 (c * kChunk + kChunk - 1 <= Tw - 2)
+            const int cs = Tw >= kChunk + 1 ? (Tw - kChunk - 1) / kChunk : 0;
+            int c = nch - 1;
+            for (; c > cs && c >= 1; --c) bchunk(c, MASK_, std::false_type{});
+            for (; c >= 1; --c) bchunk(c, MASK_, std::true_type{});
+            bchunk(0, MASK_, std::false_type{});
         };
         if (full) backward(std::false_type{});
         else backward(std::true_type{});
