@@ -57,8 +57,13 @@ __device__ __forceinline__ f64x4 mfma_f64(double a, double b, f64x4 c) {
     return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
 }
 
-template <int NT, bool FWD_ONLY>
+// DET (deterministic-reduction mode): no floating-point atomics; every statistic of the block's
+// prefix [0, off_bnum) is owned by exactly one lane, accumulated in registers in a fixed order and
+// stored once into the workgroup's partial a.part[block][off_bnum] (k_det_reduce sums the partials in
+// workgroup order; the B numerator is the gather's, deterministic already).
+template <int NT, bool FWD_ONLY, bool DET = false>
 __global__ void __launch_bounds__(NT * 64, 2) k_estep_mfma(EArgs a) {  // 2 waves per SIMD: <= 256 VGPRs
+    static_assert(!(DET && FWD_ONLY), "deterministic mode is an E-step option");
     constexpr int NP = 16 * NT, KB = 4 * NT, IMG = NP * kXs;
     extern __shared__ double smem[];
     double *X0 = smem;                                   // [2][NP][kXs]: z (forward) / V (backward)
@@ -232,6 +237,7 @@ __global__ void __launch_bounds__(NT * 64, 2) k_estep_mfma(EArgs a) {  // 2 wave
     if constexpr (!FWD_ONLY) if (!(a.ablate & 2)) {
         // ------------- backward fused with gamma / xi / M-step numerators (:370-410, :474-485) -------------
         double *accb = a.copies + (long long)(blockIdx.x % a.ncopies) * a.copy_len;
+        double dgall[4] = {0.0, 0.0, 0.0, 0.0}, dpin[4] = {0.0, 0.0, 0.0, 0.0};  // DET: this lane's sums
         const double inv_p = alive ? 1.0 / phat : 0.0;  // beta_hat_{T-1}: folds 1/P (:392, :407)
         // gamma_{T-1} = z_{T-1} / P (:392 at t = T-1): its gamma row, gamma_den_all, pi_num when T = 1
         {
@@ -243,7 +249,10 @@ __global__ void __launch_bounds__(NT * 64, 2) k_estep_mfma(EArgs a) {  // 2 wave
             for (int r = 0; r < 4; ++r) {
                 const int j = 16 * m + g + 4 * r;
                 const double x1 = rowsum(gT[r]), x2 = rowsum(T == 1 ? gT[r] : 0.0);
-                if (s == 0 && j < N) {
+                if constexpr (DET) {
+                    dgall[r] = x1;
+                    dpin[r] = x2;
+                } else if (s == 0 && j < N) {
                     if (x1 != 0.0) unsafeAtomicAdd(&accb[a.off_gall + j], x1);
                     if (x2 != 0.0) unsafeAtomicAdd(&accb[j], x2);  // pi_num at offset 0
                 }
@@ -320,7 +329,8 @@ __global__ void __launch_bounds__(NT * 64, 2) k_estep_mfma(EArgs a) {  // 2 wave
                 for (int r = 0; r < 4; ++r) {
                     const int j = 16 * m + g + 4 * r;
                     const double x = rowsum(gm[r]);
-                    if (s == 0 && j < N && x != 0.0) unsafeAtomicAdd(&accb[j], x);
+                    if constexpr (DET) dpin[r] += x;
+                    else if (s == 0 && j < N && x != 0.0) unsafeAtomicAdd(&accb[j], x);
                 }
             }
         };
@@ -366,12 +376,15 @@ __global__ void __launch_bounds__(NT * 64, 2) k_estep_mfma(EArgs a) {  // 2 wave
         if (full) backward(std::false_type{});
         else backward(std::true_type{});
         // ---- flush: xi = a_ij S_ij; gamma sums reduced over the tile's sequences ----
+        double *part = DET ? a.part + (long long)blockIdx.x * a.off_bnum : nullptr;
 #pragma unroll
         for (int mj = 0; mj < NT; ++mj)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int i = 16 * m + g + 4 * r, jj = 16 * mj + (lane & 15);
-                if (i < N && jj < N && S[mj][r] != 0.0) {
+                if constexpr (DET) {
+                    if (i < N && jj < N) part[a.off_S + (long long)i * N + jj] = S[mj][r] * a.A[i * N + jj];
+                } else if (i < N && jj < N && S[mj][r] != 0.0) {
                     const double x = S[mj][r] * a.A[i * N + jj];
                     if (x != 0.0) unsafeAtomicAdd(&accb[a.off_S + (long long)i * N + jj], x);
                 }
@@ -380,7 +393,13 @@ __global__ void __launch_bounds__(NT * 64, 2) k_estep_mfma(EArgs a) {  // 2 wave
         for (int r = 0; r < 4; ++r) {
             const double x0 = rowsum(gex[r]);
             const int j = 16 * m + g + 4 * r;
-            if (s == 0 && j < N && x0 != 0.0) {
+            if constexpr (DET) {
+                if (s == 0 && j < N) {
+                    part[j] = dpin[r];
+                    part[a.off_gex + j] = x0;
+                    part[a.off_gall + j] = dgall[r] + x0;
+                }
+            } else if (s == 0 && j < N && x0 != 0.0) {
                 unsafeAtomicAdd(&accb[a.off_gex + j], x0);
                 unsafeAtomicAdd(&accb[a.off_gall + j], x0);  // gamma_den_all = excl + the last frames
             }

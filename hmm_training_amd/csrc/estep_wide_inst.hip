@@ -6,10 +6,11 @@
 namespace hmmbw {
 
 Kernels wide_kernels(int NP) {
-    if (NP == 32) return Kernels{k_estep_mfma<2, false>, k_estep_mfma<2, true>};
-    if (NP == 48) return Kernels{k_estep_mfma<3, false>, k_estep_mfma<3, true>};
-    if (NP == 64) return Kernels{k_estep_mfma<4, false>, k_estep_mfma<4, true>};
-    return Kernels{};
+    Kernels k;
+    if (NP == 32) k = Kernels{k_estep_mfma<2, false>, k_estep_mfma<2, true>, nullptr, nullptr, k_estep_mfma<2, false, true>};
+    if (NP == 48) k = Kernels{k_estep_mfma<3, false>, k_estep_mfma<3, true>, nullptr, nullptr, k_estep_mfma<3, false, true>};
+    if (NP == 64) k = Kernels{k_estep_mfma<4, false>, k_estep_mfma<4, true>, nullptr, nullptr, k_estep_mfma<4, false, true>};
+    return k;
 }
 
 BnumFn bnum_gather_kernel() { return k_bnum_gather; }

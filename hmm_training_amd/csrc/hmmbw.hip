@@ -191,7 +191,7 @@ struct hmmbw_ctx {
     double *d_copies = nullptr;   // [3][ncopies][copy_len] E-step accumulators (iteration e uses e % 3)
     int ncopies = 2;              // HMMBW_OPT_STAT_COPIES default: halves the flush atomics per address (measured -3 %)
     bool merge_mstep = true;      // run each M-step in the prologue of the next E-step launch
-    bool det = false;             // HMMBW_OPT_DETERMINISTIC: no floating-point atomics (small kernels, LDS tables)
+    bool det = false;             // HMMBW_OPT_DETERMINISTIC: no floating-point atomics (LDS-table or wide kernels)
     double *d_part = nullptr;     // det: per-workgroup partial statistics [blocks][off_bnum]
     bool armed = false;
     long long e_count = 0;        // E-step launches since the statistics were last cleared
@@ -413,7 +413,7 @@ int plan_estep(hmmbw_ctx *c, bool fwd_only, const IterState *state, double *copi
         p.lds = sizeof(double) * ((fwd_only ? 2 * (size_t)c->NP * 17 : 4 * (size_t)c->NP * 17 + (size_t)nt * 4 * nt * 64) +
                                   (size_t)nt * 16 + 16);
         const Kernels kw = wide_kernels(c->NP);
-        p.fn = fwd_only ? kw.score : kw.estep;
+        p.fn = fwd_only ? kw.score : (c->det ? kw.det_estep : kw.estep);
         p.block = (unsigned)(nt * kWave);
         if (!p.fn) return fail(HMMBW_E_UNSUPPORTED, "no wide kernel for N");
     } else {
@@ -461,6 +461,11 @@ int launch_estep(hmmbw_ctx *c, bool fwd_only, const IterState *state, double *co
     }
     if (int rc = launch_lds(p.fn, p.grid, p.lds, c->stream, a, p.block)) return rc;
     if (c->wide && !fwd_only) {  // B numerator: per-symbol gather of the gamma rows (estep_mfma.hpp)
+        if (c->det) {  // deterministic mode: the other statistics from the partials, in workgroup order
+            const long long n = c->off_bnum();
+            hipLaunchKernelGGL(k_det_reduce, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, c->stream, c->d_part,
+                               (long long)p.grid, n, a.copies, a.state);
+        }
         hipLaunchKernelGGL(bnum_gather_kernel(), dim3((unsigned)c->K), dim3(256), 0, c->stream, c->d_gam,
                            c->d_brows, c->d_bptr, c->NP, c->N, 1, a.copies + c->off_bnum(), a.state);
         HIP_TRY(hipGetLastError());
@@ -807,6 +812,7 @@ int hmmbw_set_observations(hmmbw_ctx *c, const int64_t *offsets, const int32_t *
         if (!rc) rc = dalloc(&c->d_gam, (size_t)std::max(cktot, 1LL));
         if (!rc) rc = dalloc(&c->d_bptr, bptr.size());
         if (!rc) rc = dalloc(&c->d_brows, brows.size());
+        if (!rc && c->det) rc = dalloc(&c->d_part, (size_t)std::max(nblocks, 1LL) * (size_t)c->off_bnum());
     } else if (c->det) {  // deterministic mode: symbol -> pack positions (gamma row = pack index), stable
         if (symtot >= (1LL << 32)) return fail(HMMBW_E_UNSUPPORTED, "too many positions for the deterministic mode");
         bptr.assign((size_t)c->K + 1, 0);
@@ -872,8 +878,8 @@ int hmmbw_set_option(hmmbw_ctx *c, int key, int64_t value) {
     }
     if (key == HMMBW_OPT_DETERMINISTIC) {
         if (c->has_obs) return fail(HMMBW_E_STATE, "set the deterministic mode before hmmbw_set_observations");
-        if (value != 0 && (c->wide || !c->lds_tables()))
-            return fail(HMMBW_E_UNSUPPORTED, "deterministic mode needs N <= 16 and the LDS emission tables");
+        if (value != 0 && !c->wide && !c->lds_tables())
+            return fail(HMMBW_E_UNSUPPORTED, "deterministic mode needs the LDS emission tables (N <= 16) or the wide path");
         c->det = value != 0;
         return HMMBW_OK;
     }
@@ -1023,10 +1029,10 @@ int hmmbw_iterate(hmmbw_ctx *c, int64_t n_iter) {
                 if (int rc = take_events(c->ar_free, &e0, &e1)) return rc;
                 HIP_TRY(hipEventRecord(e0, c->stream));
             }
-            if (c->world > 1) {  // a 1-rank sum is the identity: RCCL would still launch copy kernels
-                ncclResult_t e = r->all_reduce(ar, ar, ar_len, ncclFloat64, ncclSum, c->comm, c->stream);
-                if (e != ncclSuccess) return rccl_fail(r, e, "ncclAllReduce");
-            }
+            // also at world 1 (RCCL's in-place 1-rank sum is a copy kernel, ~2 us): the 1-rank
+            // communicator tests then exercise the same ncclAllReduce call as an 8-GPU run
+            ncclResult_t e = r->all_reduce(ar, ar, ar_len, ncclFloat64, ncclSum, c->comm, c->stream);
+            if (e != ncclSuccess) return rccl_fail(r, e, "ncclAllReduce");
             if (e1) {
                 HIP_TRY(hipEventRecord(e1, c->stream));
                 c->ar_pending.push_back(e0);

@@ -17,7 +17,7 @@ using GroupFn = void (*)(GroupArgs);
 struct Kernels {
     KernelFn estep = nullptr, score = nullptr;
     GroupFn group_estep = nullptr, group_score = nullptr;  // grouped launches (LDS tables only)
-    KernelFn det_estep = nullptr;                          // deterministic-reduction E-step (LDS tables only)
+    KernelFn det_estep = nullptr;                          // deterministic-reduction E-step (LDS tables, wide)
 };
 
 // E-step and scorer kernels for N states (1 <= N <= 16), left-to-right or dense, with or without the

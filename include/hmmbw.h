@@ -163,9 +163,10 @@ int hmmbw_score(hmmbw_ctx *ctx, double *out);
 #define HMMBW_OPT_MERGE_MSTEP 4
 /* 1: deterministic-reduction mode, bitwise-identical results run to run (no floating-point atomics):
  * gamma goes to per-position rows summed per symbol in a fixed order, and the other statistics are
- * per-workgroup partials summed in workgroup order.  About twice the E-step time.  Small state counts
- * (N <= 16) with the LDS emission tables only (HMMBW_E_UNSUPPORTED otherwise); set it before
- * hmmbw_set_observations (HMMBW_E_STATE after).  Default 0. */
+ * per-workgroup partials summed in workgroup order.  About twice the E-step time on the small
+ * kernels; the wide path (16 < N <= 64) already gathers gamma rows, so there it only replaces the
+ * other statistics' atomics.  Small state counts need the LDS emission tables (HMMBW_E_UNSUPPORTED
+ * otherwise); set it before hmmbw_set_observations (HMMBW_E_STATE after).  Default 0. */
 #define HMMBW_OPT_DETERMINISTIC 7
 int hmmbw_set_option(hmmbw_ctx *ctx, int key, int64_t value);
 

@@ -37,11 +37,15 @@ def run(obs, pi, A, B, N, K, iters, det, merge=True):
         return np.array(trace), p, a, b, e.loglik()
 
 
-@pytest.mark.parametrize("N,K,topology", [(8, 256, "left_to_right"), (8, 256, "dense"), (5, 64, "dense"),
-                                          (3, 32, "left_to_right"), (13, 100, "dense")])
-def test_deterministic_runs_are_bitwise_equal_and_match_oracle(oracle, N, K, topology):
+@pytest.mark.parametrize("N,K,topology,R", [(8, 256, "left_to_right", 3000), (8, 256, "dense", 3000),
+                                            (5, 64, "dense", 3000), (3, 32, "left_to_right", 3000),
+                                            (13, 100, "dense", 3000),
+                                            # wide path (fp64 MFMA, k_estep_mfma<NT, false, true>)
+                                            (40, 64, "dense", 150), (64, 1024, "dense", 120),
+                                            (20, 50, "left_to_right", 150)])
+def test_deterministic_runs_are_bitwise_equal_and_match_oracle(oracle, N, K, topology, R):
     from hmm_training_amd.engine import to_csr
-    obs, pi, A, B = problem(N, K, 3000, topology, 41 + N)
+    obs, pi, A, B = problem(N, K, R, topology, 41 + N)
     r1 = run(obs, pi, A, B, N, K, 4, True)
     r2 = run(obs, pi, A, B, N, K, 4, True)
     for x, y in zip(r1, r2):
@@ -62,7 +66,7 @@ def test_deterministic_option_rules():
     from hmm_training_amd._lib import OPT_DETERMINISTIC, HMMBWError, lib
     from hmm_training_amd.engine import BaumWelchEngine
     with pytest.raises(HMMBWError):
-        BaumWelchEngine(40, 64, deterministic=True)  # wide path: unsupported
+        BaumWelchEngine(16, 4096, deterministic=True)  # emission tables too large for LDS: unsupported
     with BaumWelchEngine(8, 256) as e:
         e.set_observations([np.array([1, 2, 3])])
         assert lib().hmmbw_set_option(e._ctx, OPT_DETERMINISTIC, 1) != 0  # after the observations
