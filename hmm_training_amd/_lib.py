@@ -32,7 +32,8 @@ EXPORTED = (
     "hmmbw_abi_version", "hmmbw_last_error", "hmmbw_device_count", "hmmbw_ctx_create", "hmmbw_ctx_destroy",
     "hmmbw_set_stream", "hmmbw_set_rank", "hmmbw_set_topology", "hmmbw_get_topology", "hmmbw_set_observations",
     "hmmbw_set_params", "hmmbw_reset_training", "hmmbw_stats_len", "hmmbw_estep", "hmmbw_mstep",
-    "hmmbw_iterate", "hmmbw_get_status", "hmmbw_get_params", "hmmbw_get_loglik", "hmmbw_score", "hmmbw_timing",
+    "hmmbw_iterate", "hmmbw_get_status", "hmmbw_status_post", "hmmbw_status_wait",
+    "hmmbw_get_params", "hmmbw_get_loglik", "hmmbw_score", "hmmbw_timing",
     "hmmbw_set_option", "hmmbw_group_create", "hmmbw_group_destroy", "hmmbw_group_iterate", "hmmbw_group_score",
     "hmmbw_group_timing", "hmmbw_vq_encode", "hmmbw_comm_unique_id", "hmmbw_comm_init",
     "hmmbw_comm_probe", "hmmbw_comm_info",
@@ -84,6 +85,9 @@ def _declare(lib):
         "hmmbw_mstep": (ctypes.c_int, [c_ctx, ctypes.c_void_p, ctypes.c_int64]),
         "hmmbw_iterate": (ctypes.c_int, [c_ctx, ctypes.c_int64]),
         "hmmbw_get_status": (ctypes.c_int, [c_ctx, P(Status), ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64]),
+        "hmmbw_status_post": (ctypes.c_int, [c_ctx, ctypes.c_int64, P(ctypes.c_int64)]),
+        "hmmbw_status_wait": (ctypes.c_int, [c_ctx, ctypes.c_int64, P(Status), ctypes.c_void_p, ctypes.c_int64,
+                                             ctypes.c_int64]),
         "hmmbw_get_params": (ctypes.c_int, [c_ctx, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
         "hmmbw_get_loglik": (ctypes.c_int, [c_ctx, ctypes.c_void_p]),
         "hmmbw_score": (ctypes.c_int, [c_ctx, ctypes.c_void_p]),

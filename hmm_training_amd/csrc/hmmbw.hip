@@ -96,6 +96,20 @@ __global__ void __launch_bounds__(256) k_mstep_staged(MArgs m) {
 }
 
 // safe_exp + normalisation of the returned parameters (:524-541)
+// Status snapshot for hmmbw_status_post: the state record and the iteration records [first, iteration)
+// written straight into pinned host memory (one small launch on the stream instead of DMA copies).
+__global__ void __launch_bounds__(256) k_snapshot(const IterState *st, const double *hist, long long first,
+                                                   IterState *hst, double *hrec) {
+    const IterState s = *st;
+    const long long n = min(max(s.iteration - first, 0LL), (long long)kHist);
+    for (long long i = threadIdx.x; i < n; i += blockDim.x) {
+        const long long k = (first + i) % kHist;
+        hrec[2 * i] = hist[2 * k];
+        hrec[2 * i + 1] = hist[2 * k + 1];
+    }
+    if (threadIdx.x == 0) *hst = s;
+}
+
 __global__ void k_finalise(const double *pi, const double *A, const double *B, int N, int K, double *out) {
     double *opi = out, *oA = out + N, *oB = out + N + N * N;
     const int tid = threadIdx.x;
@@ -188,6 +202,15 @@ struct hmmbw_ctx {
     IterState *d_state = nullptr;  // [2]: the current slot is scur; every M-step writes the other
     int scur = 0;
     double *d_hist = nullptr;
+    // hmmbw_status_post / _wait: two pinned snapshots (state + record ring) taken on the stream
+    struct Snap {
+        hipEvent_t ev = nullptr;
+        IterState *st = nullptr;
+        double *hist = nullptr;  // records [first, st->iteration)
+        long long first = 0;
+        long long ticket = -1;
+    } snaps[2];
+    long long snap_next = 0;
     double *d_copies = nullptr;   // [3][ncopies][copy_len] E-step accumulators (iteration e uses e % 3)
     int ncopies = 2;              // HMMBW_OPT_STAT_COPIES default: halves the flush atomics per address (measured -3 %)
     bool merge_mstep = true;      // run each M-step in the prologue of the next E-step launch
@@ -653,6 +676,11 @@ int hmmbw_ctx_destroy(hmmbw_ctx *c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     else (void)hipDeviceSynchronize();
     dfree(c->d_pi); dfree(c->d_A); dfree(c->d_B); dfree(c->d_Bt); dfree(c->d_out);
+    for (auto &sn : c->snaps) {
+        if (sn.ev) (void)hipEventDestroy(sn.ev);
+        if (sn.st) (void)hipHostFree(sn.st);
+        if (sn.hist) (void)hipHostFree(sn.hist);
+    }
     dfree(c->d_state); dfree(c->d_hist); dfree(c->d_copies); dfree(c->d_ext); dfree(c->d_xbuf); dfree(c->d_ctr);
     if (c->comm) {
         Rccl *r = nullptr;
@@ -1084,6 +1112,14 @@ int hmmbw_iterate(hmmbw_ctx *c, int64_t n_iter) {
     return HMMBW_OK;
 }
 
+static void fill_status(const IterState &h, hmmbw_status *st) {
+    st->iterations = h.iteration;
+    st->done = h.done;
+    st->converged = h.converged;
+    st->last_log_likelihood = h.last_L;
+    st->last_diff = h.last_diff;
+}
+
 int hmmbw_get_status(hmmbw_ctx *c, hmmbw_status *st, hmmbw_iter_record *rec, int64_t first, int64_t count) {
     if (!c || !st) return fail(HMMBW_E_INVALID, "null argument");
     if (int rc = set_device(c)) return rc;
@@ -1094,11 +1130,7 @@ int hmmbw_get_status(hmmbw_ctx *c, hmmbw_status *st, hmmbw_iter_record *rec, int
     if (rec && count > 0)
         HIP_TRY(hipMemcpyAsync(hist.data(), c->d_hist, sizeof(double) * hist.size(), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
-    st->iterations = h.iteration;
-    st->done = h.done;
-    st->converged = h.converged;
-    st->last_log_likelihood = h.last_L;
-    st->last_diff = h.last_diff;
+    fill_status(h, st);
     if (rec && count > 0) {
         if (first < 0 || first + count > h.iteration || first < h.iteration - kHist)
             return fail(HMMBW_E_INVALID, "requested iteration records are not available");
@@ -1106,6 +1138,55 @@ int hmmbw_get_status(hmmbw_ctx *c, hmmbw_status *st, hmmbw_iter_record *rec, int
             const int64_t k = (first + i) % kHist;
             rec[i].log_likelihood = hist[2 * k];
             rec[i].diff = hist[2 * k + 1];
+        }
+    }
+    return HMMBW_OK;
+}
+
+int hmmbw_status_post(hmmbw_ctx *c, int64_t first, int64_t *ticket) {
+    if (!c || !ticket) return fail(HMMBW_E_INVALID, "null argument");
+    if (first < 0) return fail(HMMBW_E_INVALID, "negative first iteration");
+    if (int rc = set_device(c)) return rc;
+    hmmbw_ctx::Snap &sn = c->snaps[c->snap_next % 2];
+    if (!sn.ev) {
+        HIP_TRY(hipEventCreateWithFlags(&sn.ev, hipEventDisableTiming));
+        // fine-grained host memory the snapshot kernel writes (visible once its event has completed)
+        const unsigned fl = hipHostMallocMapped | hipHostMallocCoherent;
+        HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&sn.st), sizeof(IterState), fl));
+        HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&sn.hist), sizeof(double) * 2 * (size_t)kHist,
+                              fl));
+    } else {
+        HIP_TRY(hipEventSynchronize(sn.ev));  // the slot's previous snapshot has landed (two posts ago)
+    }
+    // no flush: a pending (merged) M-step stays pending, so the snapshot holds the records of every
+    // iteration enqueued so far except the last one
+    hipLaunchKernelGGL(k_snapshot, dim3(1), dim3(256), 0, c->stream, c->state(), c->d_hist, (long long)first, sn.st,
+                       sn.hist);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(sn.ev, c->stream));
+    sn.first = first;
+    sn.ticket = c->snap_next++;
+    *ticket = sn.ticket;
+    return HMMBW_OK;
+}
+
+int hmmbw_status_wait(hmmbw_ctx *c, int64_t ticket, hmmbw_status *st, hmmbw_iter_record *rec, int64_t first,
+                      int64_t count) {
+    if (!c || !st) return fail(HMMBW_E_INVALID, "null argument");
+    if (ticket < 0 || ticket >= c->snap_next || ticket < c->snap_next - 2)
+        return fail(HMMBW_E_INVALID, "status ticket is not one of the last two posted");
+    if (int rc = set_device(c)) return rc;
+    hmmbw_ctx::Snap &sn = c->snaps[ticket % 2];
+    HIP_TRY(hipEventSynchronize(sn.ev));  // this snapshot only, not the work enqueued after it
+    const IterState h = *sn.st;
+    fill_status(h, st);
+    if (rec && count > 0) {
+        if (first < sn.first || first + count > h.iteration || first + count > sn.first + kHist)
+            return fail(HMMBW_E_INVALID, "requested iteration records are not in this snapshot");
+        for (int64_t i = 0; i < count; ++i) {
+            const int64_t k = first + i - sn.first;
+            rec[i].log_likelihood = sn.hist[2 * k];
+            rec[i].diff = sn.hist[2 * k + 1];
         }
     }
     return HMMBW_OK;

@@ -15,6 +15,7 @@ otherwise (gloo, or HMMBW_NATIVE_COMM=0) the all-reduce goes through torch.distr
 """
 from __future__ import annotations
 
+import collections
 import ctypes
 import json
 import os
@@ -251,33 +252,69 @@ class BaumWelchEngine:
         if mfh is not None:
             self.timing(1)
             self.comm_info(reset=True)
-        reported, chunk = 0, 1
+        # Pipelined: chunk k + 1 is queued before chunk k's status snapshot is read (hmmbw_status_post
+        # / _wait wait for the snapshot only), so the device never idles on a host round trip.  The
+        # snapshots lag one iteration (the last iteration's M-step is merged into the next launch);
+        # iterations queued past the stop rule are device-side no-ops, and the final synchronous
+        # status covers the rest.  Every rank takes the same decisions (identical device states).
+        max_it = int(max_iterations)
+        reported, chunk, queued = 0, 1, 0
+        inflight = collections.deque()  # (ticket, iterations queued up to it)
+        t_last = time.perf_counter()
+        st = None
         try:
             while True:
-                st, _ = self.status()
-                if st.done:
+                if queued < max_it:
+                    n = min(chunk, max_it - queued)
+                    self.enqueue_iterations(n, stats, group)
+                    queued += n
+                    chunk = min(chunk * 2, max_chunk)
+                    tk = ctypes.c_int64()
+                    check(self._lib.hmmbw_status_post(self._ctx, reported, ctypes.byref(tk)))
+                    inflight.append((tk.value, queued))
+                if not inflight:
                     break
-                n = max(1, min(chunk, int(max_iterations) - st.iterations))
-                t0 = time.perf_counter()
-                self.enqueue_iterations(n, stats, group)
-                st, recs = self.status(reported, 0)
-                wall = time.perf_counter() - t0
+                if len(inflight) < 2 and queued < max_it:
+                    continue  # keep two snapshots' worth of work queued
+                ticket, upto = inflight.popleft()
+                st, recs = self._wait_status(ticket, reported)
+                now = time.perf_counter()
                 new = st.iterations - reported
-                recs = self.status(reported, new)[1] if new > 0 and (on_iteration is not None or mfh) else []
                 if on_iteration is not None:
                     for k, (L, d) in enumerate(recs):
                         on_iteration(reported + k, L, d)
                 if mfh is not None and new > 0:
-                    self._write_metrics(mfh, reported, recs, wall, n)
+                    self._write_metrics(mfh, reported, recs, now - t_last, new)
+                t_last = now
                 reported = st.iterations
-                chunk = min(chunk * 2, max_chunk)
                 if st.done:
                     break
+            st, recs = self.status(reported, 0)  # synchronous: flushes the pending M-step
+            new = st.iterations - reported
+            if new > 0:
+                recs = self.status(reported, new)[1]
+                if on_iteration is not None:
+                    for k, (L, d) in enumerate(recs):
+                        on_iteration(reported + k, L, d)
+                if mfh is not None:
+                    self._write_metrics(mfh, reported, recs, time.perf_counter() - t_last, new)
         finally:
             if mfh is not None:
                 self.timing(0)
                 mfh.close()
         return st
+
+    def _wait_status(self, ticket: int, first: int) -> Tuple[Status, List[Tuple[float, float]]]:
+        """Status snapshot `ticket` (hmmbw_status_wait) with the records of iterations [first, ...)."""
+        st = Status()
+        check(self._lib.hmmbw_status_wait(self._ctx, int(ticket), ctypes.byref(st), None, 0, 0))
+        count = int(st.iterations) - int(first)
+        if count <= 0:
+            return st, []
+        recs = (IterRecord * count)()
+        check(self._lib.hmmbw_status_wait(self._ctx, int(ticket), ctypes.byref(st),
+                                          ctypes.cast(recs, ctypes.c_void_p), int(first), count))
+        return st, [(recs[i].log_likelihood, recs[i].diff) for i in range(count)]
 
     def _write_metrics(self, fh, first: int, recs, wall_s: float, enqueued: int) -> None:
         """One JSON line per iteration of the chunk: L and diff (hmm_training.py:503-514), the chunk's

@@ -135,6 +135,20 @@ int hmmbw_comm_info(hmmbw_ctx *ctx, int *n_ranks, double *total_ms, int64_t *cou
 int hmmbw_get_status(hmmbw_ctx *ctx, hmmbw_status *status, hmmbw_iter_record *records, int64_t first,
                      int64_t count);
 
+/* ASYNC. Snapshot the status and the iteration records [first, iterations) on the context stream
+ * into pinned host memory (one small kernel; no M-step flush: with merged M-steps the snapshot covers
+ * every iteration enqueued before it except the last) and return its ticket.  Lets a host loop keep the next chunk of iterations
+ * queued while it reads the previous chunk's status (the drop-in train loop, hmm_training.py
+ * :346-514; iterations enqueued past convergence are device-side no-ops).  Two snapshots are kept:
+ * posting a third first waits for the oldest to land. */
+int hmmbw_status_post(hmmbw_ctx *ctx, int64_t first, int64_t *ticket);
+
+/* Waits for snapshot `ticket` (one of the last two posted) only, not for the work queued after it;
+ * then fills status and the records [first, first+count), which must lie inside the snapshot's
+ * [first posted, iterations). */
+int hmmbw_status_wait(hmmbw_ctx *ctx, int64_t ticket, hmmbw_status *status, hmmbw_iter_record *records,
+                      int64_t first, int64_t count);
+
 /* SYNC. Current parameters.  normalise=1 applies the reference's return path (safe_exp then
  * pi/sum(pi), row-normalise A and B rows with positive sums, :524-541); normalise=0 returns the
  * unnormalised working parameters (exp of the reference's log_pi/log_a/log_b matrices). */
