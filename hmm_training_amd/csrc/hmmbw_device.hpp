@@ -869,8 +869,17 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
         }
     }
 
-    // per-block (max, sum exp) of log P for the convergence scalar
     __syncthreads();
+    // the B-numerator histogram's atomics first: their round trips overlap the reductions below
+    if constexpr (!FWD_ONLY && !DET && LDSTAB) if (!(a.ablate & 1)) {
+        for (int idx = tid; idx < K * G; idx += blockDim.x) {
+            const int k = idx / G, jj = idx - k * G;
+            if (jj >= N) continue;
+            const double x = sH[((size_t)k * GP + jj) * 2];
+            if (x != 0.0) unsafeAtomicAdd(&accb[a.off_bnum + (long long)k * N + jj], x);
+        }
+    }
+    // per-block (max, sum exp) of log P for the convergence scalar
     block_ll_partial(logp_lane, ll_valid, sRed, a.llpart + 2 * bid);
     PHASE(4);
     // fused multi-rank launch: thread 0 counts this workgroup's pair in during the statistics flush (the
@@ -929,13 +938,6 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
         if constexpr (DET) {
             __syncthreads();
             for (long long i = tid; i < a.off_bnum; i += blockDim.x) a.part[bid * a.off_bnum + i] = sPart[i];
-        } else if constexpr (LDSTAB) {
-            for (int idx = tid; idx < K * G; idx += blockDim.x) {
-                const int k = idx / G, jj = idx - k * G;
-                if (jj >= N) continue;
-                const double x = sH[((size_t)k * GP + jj) * 2];
-                if (x != 0.0) unsafeAtomicAdd(&accb[a.off_bnum + (long long)k * N + jj], x);
-            }
         }
     }
     PHASE(5);
