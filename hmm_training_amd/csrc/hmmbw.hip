@@ -95,7 +95,6 @@ __global__ void __launch_bounds__(256) k_mstep_staged(MArgs m) {
     mstep_staged<false>(m, sSt);
 }
 
-// safe_exp + normalisation of the returned parameters (:524-541)
 // Status snapshot for hmmbw_status_post: the state record and the iteration records [first, iteration)
 // written straight into pinned host memory (one small launch on the stream instead of DMA copies).
 __global__ void __launch_bounds__(256) k_snapshot(const IterState *st, const double *hist, long long first,
@@ -110,6 +109,7 @@ __global__ void __launch_bounds__(256) k_snapshot(const IterState *st, const dou
     if (threadIdx.x == 0) *hst = s;
 }
 
+// safe_exp + normalisation of the returned parameters (:524-541)
 __global__ void k_finalise(const double *pi, const double *A, const double *B, int N, int K, double *out) {
     double *opi = out, *oA = out + N, *oB = out + N + N * N;
     const int tid = threadIdx.x;
