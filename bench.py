@@ -70,8 +70,8 @@ WORKLOADS = {  # name: (sequences per GPU, T, N, K)
 def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=50)
-    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--steps", type=int, default=200)
+    p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--workload", default="auto", choices=["auto", *WORKLOADS],
                    help="auto: cfg3 on one GPU, cfg4 shards (12,500 per GPU) on several")
     p.add_argument("--R", type=int, default=None, help="sequences per GPU (overrides the workload)")
