@@ -24,14 +24,16 @@ def rccl_path():
     return p.encode() if os.path.exists(p) else None
 
 
-@pytest.mark.parametrize("topology,maxit,N,K,eps,copies", [
-    ("left_to_right", 8, 8, 256, 1e-6, None),   # fused path: E-step into the all-reduce buffer
-    ("dense", 5, 8, 256, 1e-6, None),
-    ("left_to_right", 40, 5, 64, 1e-3, 1),      # converges before maxit (device-side stop rule)
-    ("dense", 4, 8, 256, 1e-6, 3),
-    ("dense", 3, 40, 96, 1e-6, None),           # wide path: estep + k_reduce_local + all-reduce
+@pytest.mark.parametrize("topology,maxit,N,K,eps,copies,det", [
+    ("left_to_right", 8, 8, 256, 1e-6, None, False),   # fused path: E-step into the all-reduce buffer
+    ("dense", 5, 8, 256, 1e-6, None, False),
+    ("left_to_right", 40, 5, 64, 1e-3, 1, False),      # converges before maxit (device-side stop rule)
+    ("dense", 4, 8, 256, 1e-6, 3, False),
+    ("dense", 3, 40, 96, 1e-6, None, False),           # wide path: estep + k_reduce_local + all-reduce
+    ("left_to_right", 6, 8, 256, 1e-6, None, True),    # deterministic mode: partials, estep path
+    ("dense", 3, 40, 96, 1e-6, None, True),            # deterministic wide path
 ])
-def test_native_comm_one_rank_matches_oracle(oracle, topology, maxit, N, K, eps, copies):
+def test_native_comm_one_rank_matches_oracle(oracle, topology, maxit, N, K, eps, copies, det):
     from hmm_training_amd._lib import check, lib
     from hmm_training_amd.engine import BaumWelchEngine
     from hmm_training_amd.hmm_training import default_initial_params
@@ -42,7 +44,7 @@ def test_native_comm_one_rank_matches_oracle(oracle, topology, maxit, N, K, eps,
     if topology == "dense":
         A = 0.5 * A + 0.5 * rng.dirichlet(np.ones(N), size=N)
     L = lib()
-    with BaumWelchEngine(N, K, device=0, stat_copies=copies) as e:
+    with BaumWelchEngine(N, K, device=0, stat_copies=copies, deterministic=det) as e:
         check(L.hmmbw_set_rank(e._ctx, 0, 1))
         e.set_observations(obs)
         e.set_params(pi, A, B)
