@@ -273,6 +273,16 @@ __device__ __forceinline__ uint4 pack_exps(const int *e) {
 
 __device__ __forceinline__ double pow2_scale(double x, int e) { return __builtin_amdgcn_ldexp(x, -e); }
 
+// 32-bit LDS byte address of a pointer into shared memory, and back (kept in one VGPR instead of
+// being re-derived from its parts)
+typedef __attribute__((address_space(3))) char lds_char;
+__device__ __forceinline__ unsigned lds_addr(const char *p) {
+    return (unsigned)(size_t)(const lds_char *)p;
+}
+__device__ __forceinline__ char *lds_ptr(unsigned a) {
+    return (char *)(lds_char *)(size_t)a;
+}
+
 // Per-block (max, sum exp(x - max)) of the sequences' log P (each sequence contributes from
 // exactly one lane with valid = true).  All threads of the block call it.
 __device__ void block_ll_partial(double lp, bool valid, double *sh, double *out) {
@@ -660,25 +670,30 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
                 for (int i = 0; i < 4; ++i) X[i] = ldset(cl - i >= 0 ? cl - i : 0);
                 Em E[2][kChunk];
                 double BU[2][kChunk];
-                auto ldrows = [&](Em (&bv)[kChunk], double (&bu)[kChunk], const uint4 &p) {
+                // LDSTAB: this lane's table-row byte offsets of a chunk's symbols, computed once when the
+                // chunk's emission rows are read (one chunk ahead) and reused by its histogram atomics
+                // (32-bit LDS byte addresses, the table base included, so the atomics need no add)
+                unsigned HA[2][kChunk];
+                auto ldrows = [&](Em (&bv)[kChunk], double (&bu)[kChunk], unsigned (&ha)[kChunk], const uint4 &p) {
 #pragma unroll
                     for (int k = 0; k < kChunk; ++k) {
+                        if constexpr (LDSTAB) ha[k] = lds_addr(pj) + (unsigned)sym_of(p, k);
                         if constexpr (PT) {
-                            bv[k] = ld_em(p, k);
+                            bv[k] = *reinterpret_cast<const double2 *>(lds_ptr(ha[k]));
                         } else {
-                            const double *r = brow(p, k);
+                            const double *r = LDSTAB ? reinterpret_cast<const double *>(lds_ptr(ha[k])) : brow(p, k);
                             bv[k] = r[0];
                             if constexpr (LR) bu[k] = r[1];  // b_{j+1}(o): the neighbour's emission
                         }
                     }
                 };
-                ldrows(E[0], BU[0], X[0].pk);
+                ldrows(E[0], BU[0], HA[0], X[0].pk);
                 double f_hi = 0.0, fu_hi = 0.0;  // scaled emissions at o_{8c+8} (from chunk c+1)
                 Em e_hi{};                       // PT: product pair at o_{8c+8} ...
                 int s_hi = 0;                    // ... and that step's scale exponent
                 auto chunk = [&](int c, const Ld &cur, const uint4 &pkn, const Em (&bv)[kChunk],
                                  const double (&bu)[kChunk], Em (&bvn)[kChunk], double (&bun)[kChunk],
-                                 auto MASK_) {
+                                 const unsigned (&hac)[kChunk], unsigned (&han)[kChunk], auto MASK_) {
                     constexpr bool MASK = decltype(MASK_)::value;
                     const uint4 &spA = cur.sp, &pkA = cur.pk;
                     int sk[kChunk];
@@ -783,7 +798,7 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
                     }
                     // next chunk's emission rows go to LDS before this chunk's histogram atomics, so
                     // they are not queued behind them
-                    ldrows(bvn, bun, pkn);
+                    ldrows(bvn, bun, han, pkn);
 #ifndef HMMBW_NO_HIST  // diagnostics build: no B-numerator histogram
                     if constexpr (DET) {
                         // gamma row of every position (position = index of the symbol in the pack layout)
@@ -795,7 +810,7 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
                         // columns), so the compiler's lgkmcnt bookkeeping stays exact
 #pragma unroll
                         for (int k = 0; k < kChunk; ++k)  // :474-485
-                            atomicAdd(reinterpret_cast<double *>(pent(pkA, k) + kHistOff), gk[k]);  // H.h of o_t
+                            atomicAdd(reinterpret_cast<double *>(lds_ptr(hac[k]) + kHistOff), gk[k]);  // H.h of o_t
                     } else if (N == G || jv) {
 #pragma unroll
                         for (int k = 0; k < kChunk; ++k)
@@ -812,7 +827,8 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
                     constexpr int rn = (r + 1) & 3;
                     __builtin_amdgcn_sched_barrier(0);  // one chunk at a time: registers stay per chunk
                     CHUNKSTAMP(1, c);
-                    chunk(c, X[r], X[rn].pk, E[r & 1], BU[r & 1], E[(r + 1) & 1], BU[(r + 1) & 1], MASK_);
+                    chunk(c, X[r], X[rn].pk, E[r & 1], BU[r & 1], E[(r + 1) & 1], BU[(r + 1) & 1], HA[r & 1],
+                          HA[(r + 1) & 1], MASK_);
                     X[r] = ldset(c >= 4 ? c - 4 : 0);  // branch-free: exact vmcnt accounting
                 };
                 using Mk = std::integral_constant<bool, RAG>;  // only the first chunk is masked in full waves
