@@ -386,7 +386,9 @@ def main(argv=None):
                                      f"torch.distributed ({args.dist_backend})") if world > 1 else None},
             "roofline": roof,
             "comm": {"rccl_comm_ranks": comm_ranks, "allreduce_us_per_iter": 1000.0 * ar_ms / ar_n if ar_n else None,
-                     "allreduce_timed": ar_n, "payload_bytes": 8 * eng.stats_len} if world > 1 else None,
+                     "allreduce_timed": ar_n,
+                     "payload_bytes": eng.comm_payload_bytes() if eng.native_comm else 8 * eng.stats_len}
+            if world > 1 else None,
             "synced": synced,
             "upload_s": upload_s,
             "loglik_last": st.last_log_likelihood,

@@ -36,7 +36,7 @@ EXPORTED = (
     "hmmbw_get_params", "hmmbw_get_loglik", "hmmbw_score", "hmmbw_timing",
     "hmmbw_set_option", "hmmbw_group_create", "hmmbw_group_destroy", "hmmbw_group_iterate", "hmmbw_group_score",
     "hmmbw_group_timing", "hmmbw_vq_encode", "hmmbw_comm_unique_id", "hmmbw_comm_init",
-    "hmmbw_comm_probe", "hmmbw_comm_info",
+    "hmmbw_comm_probe", "hmmbw_comm_info", "hmmbw_comm_payload",
 )
 OPT_SAFE_SCALING = 1
 OPT_ABLATE = 2
@@ -102,6 +102,7 @@ def _declare(lib):
                                            ctypes.c_int64]),
         "hmmbw_comm_info": (ctypes.c_int, [c_ctx, P(ctypes.c_int), P(ctypes.c_double), P(ctypes.c_int64),
                                            ctypes.c_int]),
+        "hmmbw_comm_payload": (ctypes.c_int, [c_ctx, P(ctypes.c_int64)]),
         "hmmbw_group_create": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, P(ctypes.c_void_p)]),
         "hmmbw_group_destroy": (ctypes.c_int, [ctypes.c_void_p]),
         "hmmbw_group_iterate": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64]),

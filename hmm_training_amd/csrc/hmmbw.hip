@@ -250,6 +250,7 @@ struct hmmbw_ctx {
     // all-reduce buffer [3][xlen] = {ncopies statistics copies, (max, sum exp) per rank}; the last
     // workgroup of each launch writes the rank's pair (d_ctr: completion counter)
     double *d_xbuf = nullptr;
+    long long ar_len_last = 0;    // doubles in the last all-reduce hmmbw_iterate enqueued
     long long xlen = 0;
     int *d_ctr = nullptr;
     // all-reduce timing (hmmbw_comm_info): event pairs around ncclAllReduce, same schedule as timing
@@ -1059,6 +1060,7 @@ int hmmbw_iterate(hmmbw_ctx *c, int64_t n_iter) {
             }
             // also at world 1 (RCCL's in-place 1-rank sum is a copy kernel, ~2 us): the 1-rank
             // communicator tests then exercise the same ncclAllReduce call as an 8-GPU run
+            c->ar_len_last = (long long)ar_len;
             ncclResult_t e = r->all_reduce(ar, ar, ar_len, ncclFloat64, ncclSum, c->comm, c->stream);
             if (e != ncclSuccess) return rccl_fail(r, e, "ncclAllReduce");
             if (e1) {
@@ -1405,6 +1407,12 @@ int hmmbw_comm_init(hmmbw_ctx *c, const char *rccl_path, const void *id, int ran
     HIP_TRY(hipMemset(c->d_ext, 0, sizeof(double) * (size_t)c->stats_len()));
     c->comm = comm;
     c->R_global = n_seq_global;
+    return HMMBW_OK;
+}
+
+int hmmbw_comm_payload(const hmmbw_ctx *c, int64_t *n_doubles) {
+    if (!c || !n_doubles) return fail(HMMBW_E_INVALID, "null argument");
+    *n_doubles = c->ar_len_last;
     return HMMBW_OK;
 }
 

@@ -371,6 +371,12 @@ class BaumWelchEngine:
         check(self._lib.hmmbw_comm_info(self._ctx, ctypes.byref(n), ctypes.byref(ms), ctypes.byref(cnt), int(reset)))
         return n.value, ms.value, cnt.value
 
+    def comm_payload_bytes(self) -> int:
+        """Bytes of the last all-reduce hmmbw_iterate enqueued on the engine communicator (0: none)."""
+        n = ctypes.c_int64()
+        check(self._lib.hmmbw_comm_payload(self._ctx, ctypes.byref(n)))
+        return 8 * n.value
+
     def close(self) -> None:
         if getattr(self, "_ctx", None):
             self._lib.hmmbw_ctx_destroy(self._ctx)

@@ -131,6 +131,11 @@ int hmmbw_comm_init(hmmbw_ctx *ctx, const char *rccl_path, const void *id, int r
  * clears the accumulated time.  Measurement only (bench.py's all-reduce microseconds per iteration). */
 int hmmbw_comm_info(hmmbw_ctx *ctx, int *n_ranks, double *total_ms, int64_t *count, int reset);
 
+/* Length in doubles of the last all-reduce hmmbw_iterate enqueued on the engine communicator (0
+ * before the first): the fused small path all-reduces its statistics copies plus one (max, sum exp)
+ * pair per rank, 256-B aligned; the other paths the packed statistics (hmmbw_stats_len). */
+int hmmbw_comm_payload(const hmmbw_ctx *ctx, int64_t *n_doubles);
+
 /* SYNC. Status plus the iteration records [first, first+count) (ring of 4096 entries). */
 int hmmbw_get_status(hmmbw_ctx *ctx, hmmbw_status *status, hmmbw_iter_record *records, int64_t first,
                      int64_t count);

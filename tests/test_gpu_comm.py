@@ -57,6 +57,12 @@ def test_native_comm_one_rank_matches_oracle(oracle, topology, maxit, N, K, eps,
         p2, A2, B2 = e.params()
         ranks, ar_ms, ar_n = e.comm_info()
         assert ranks == 1 and ar_n >= st.iterations and ar_ms > 0  # chunks past convergence still all-reduce
+        copy_len = N + N * N + 2 * N + K * N
+        if N <= 16 and not det:  # fused: the copies + one (max, sum exp) pair per rank, 256-B aligned
+            nc = copies or 2
+            assert e.comm_payload_bytes() == 8 * (-(-(nc * copy_len + 2) // 32) * 32)
+        else:
+            assert e.comm_payload_bytes() == 8 * e.stats_len
     off = np.concatenate([[0], np.cumsum([len(o) for o in obs])]).astype(np.int64)
     ref = oracle.hmm_training(off, np.concatenate(obs).astype(np.int64), N, K, eps, maxit, pi, A, B)
     assert st.iterations == ref.iterations
