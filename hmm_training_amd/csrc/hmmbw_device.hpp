@@ -446,6 +446,11 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
         double *ckw = a.ckpt + (FWD_ONLY ? 0 : a.L.wave_ckoff[wave]) + lane;
         uint4 *spw = a.spack + (FWD_ONLY ? 0 : a.L.wave_spoff[wave]) + u;
         const bool jv = j < N;
+        // shortest sequence of the wave (0 with a padding slot): in a ragged wave the chunks every
+        // lane is still inside of run unmasked
+        int Tmin = T;
+#pragma unroll
+        for (int m = G; m < kWave; m <<= 1) Tmin = min(Tmin, __shfl_xor(Tmin, m));
 
         // transition coefficients of this lane (state j)
         double acol[LR ? 1 : N], arow[LR ? 1 : N];
@@ -609,6 +614,14 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
             const int lim = RAG ? nch : ((Tw % kChunk) != 0 ? nch - 1 : nch);  // chunks [1, lim) unmasked (full)
             int c = 1;
             using Mk = std::integral_constant<bool, RAG>;
+            if constexpr (RAG) {  // ragged wave: chunks [1, Tmin / 8) have every lane active
+                for (; c + 4 <= Tmin / kChunk; c += 4) {
+                    body(c, I1{}, F0{}, F0{});
+                    body(c + 1, I2{}, F0{}, F0{});
+                    body(c + 2, I3{}, F0{}, F0{});
+                    body(c + 3, I0{}, F0{}, F0{});
+                }
+            }
             for (; c + 4 <= lim; c += 4) {
                 body(c, I1{}, Mk{}, F0{});
                 body(c + 1, I2{}, Mk{}, F0{});
@@ -841,6 +854,24 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
                     // steady loop: 4 chunks per trip, no branches around the loads or the LDS
                     // atomics, so the compiler's vmcnt / lgkmcnt waits stay exact
                     int c = cl - 1;
+                    if constexpr (RAG) {
+                        // ragged wave: masked while a trip holds some lane's last frames, then the
+                        // chunks with t <= Tmin - 2 for every lane (c <= (Tmin - 9) / 8) unmasked
+                        const int cr = Tmin >= kChunk + 1 ? (Tmin - kChunk - 1) / kChunk : -1;
+                        for (; c >= 3 && c > cr; c -= 4) {
+                            body(c, I1{}, Mk{});
+                            body(c - 1, I2{}, Mk{});
+                            body(c - 2, I3{}, Mk{});
+                            body(c - 3, I0{}, Mk{});
+                        }
+                        using U0 = std::false_type;
+                        for (; c >= 3; c -= 4) {
+                            body(c, I1{}, U0{});
+                            body(c - 1, I2{}, U0{});
+                            body(c - 2, I3{}, U0{});
+                            body(c - 3, I0{}, U0{});
+                        }
+                    }
                     for (; c >= 3; c -= 4) {
                         body(c, I1{}, Mk{});
                         body(c - 1, I2{}, Mk{});
