@@ -446,9 +446,11 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
         double *ckw = a.ckpt + (FWD_ONLY ? 0 : a.L.wave_ckoff[wave]) + lane;
         uint4 *spw = a.spack + (FWD_ONLY ? 0 : a.L.wave_spoff[wave]) + u;
         const bool jv = j < N;
-        // shortest sequence of the wave (0 with a padding slot): in a ragged wave the chunks every
-        // lane is still inside of run unmasked
-        int Tmin = T;
+        // shortest sequence of the wave: in a ragged wave the chunks every lane is still inside of run
+        // unmasked.  Padding slots (T = 0; empty sequences are rejected at the ABI) do not count: their
+        // z starts at 0 in the (masked) first chunk and their beta at 1/P = 0, so every term they
+        // add in an unmasked chunk is an exact zero.
+        int Tmin = T > 0 ? T : INT_MAX;
 #pragma unroll
         for (int m = G; m < kWave; m <<= 1) Tmin = min(Tmin, __shfl_xor(Tmin, m));
 
