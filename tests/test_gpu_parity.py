@@ -137,12 +137,9 @@ SWEEP += [(8, 700, "dense"), (8, 700, "left_to_right"), (16, 300, "dense"), (17,
 SAFE_SWEEP = [(N, K, topo) for (N, K, topo) in SWEEP if N in (2, 5, 8, 16)]
 
 
-@pytest.mark.parametrize("safe", [False, True])
-@pytest.mark.parametrize("N,K,topology", SWEEP)
+@pytest.mark.parametrize("N,K,topology,safe", [c + (False,) for c in SWEEP] + [c + (True,) for c in SAFE_SWEEP])
 def test_training_vs_oracle_random(N, K, topology, safe, oracle):
     from hmm_training_amd.engine import BaumWelchEngine, to_csr
-    if safe and (N, K, topology) not in SAFE_SWEEP:
-        pytest.skip("safe-scaling mode swept on a subset")
     rng = np.random.default_rng(1000 * N + K)
     obs, pi, A, B = random_problem(rng, N, K, R=37, tmax=90, topology=topology)
     off, sym = to_csr(obs)
@@ -328,19 +325,18 @@ def test_engine_variants_match_reference(case, merge, copies):
 
 
 @pytest.mark.parametrize("case", ["n8_k256_t200", "converge", "zero_prob_seq", "dense_n16", "n64_k1024_tiny"])
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 5])
 def test_multirank_estep_mstep_in_process(case, world):
     """The multi-rank path (hmmbw_estep -> sum of the packed statistics -> hmmbw_mstep) with `world`
     engines in one process on cuda:0; the all-reduce is a torch sum.  Must match the reference run
-    on the unsharded data (hmm_training.py:351-514)."""
+    on the unsharded data (hmm_training.py:351-514).  Ranks with an empty shard (more ranks than
+    sequences: n64_k1024_tiny holds 2) contribute zero statistics and still run every M-step."""
     import torch
     from hmm_training_amd.engine import BaumWelchEngine, shard_bounds
     d = load(case)
     N, M = int(d["N"]), int(d["M"])
     obs = observations(d)
     bounds = shard_bounds([len(o) for o in obs], world)
-    if any(hi <= lo for lo, hi in bounds):
-        pytest.skip("a rank would be empty")
     engines, bufs = [], []
     for r, (lo, hi) in enumerate(bounds):
         e = BaumWelchEngine(N, M, rank=r, world_size=world)
