@@ -99,6 +99,13 @@ def test_csr_and_shards():
         assert all(b[i][1] == b[i + 1][0] for i in range(world - 1))
         loads = [lengths[s:e].sum() for s, e in b]
         assert max(loads) - min(loads) <= 2 * lengths.max()
+    # more ranks than sequences: every sequence lands on exactly one rank, the rest get empty shards
+    for R, world in ((0, 2), (1, 8), (2, 3), (3, 8)):
+        b = shard_bounds([7] * R, world)
+        assert len(b) == world and b[0][0] == 0 and b[-1][1] == R
+        assert all(s <= e for s, e in b) and all(b[i][1] == b[i + 1][0] for i in range(world - 1))
+        assert sum(e - s for s, e in b) == R
+    assert to_csr([])[0].tolist() == [0]
 
 
 def test_stats_layout_roundtrip():
