@@ -87,7 +87,8 @@ def parse(argv=None):
     p.add_argument("--no-synced", action="store_true", help="skip the synced-protocol and drop-in measurements")
     p.add_argument("--seed", type=int, default=None)
     p.add_argument("--no-kernel-timing", action="store_true", help="skip the HIP events")
-    p.add_argument("--timing-every", type=int, default=5, help="time every k-th E-step launch")
+    p.add_argument("--timing-batch", type=int, default=20,
+                   help="E-step launches timed one by one (HIP events) after the timed region")
     p.add_argument("--deterministic", action="store_true", help="fixed-order reductions (no fp atomics), bitwise reproducible")
     p.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) on MI355X; gloo only for tests")
     p.add_argument("--dry-run", action="store_true", help="launcher + rendezvous + timing skeleton, no GPU work")
@@ -167,6 +168,26 @@ def find_traffic(cfg_key):
             continue
         if d.get("config_key") == cfg_key and d.get("hbm_bytes_per_launch"):
             best = (float(d["hbm_bytes_per_launch"]), os.path.relpath(path, ROOT))
+    return best
+
+
+SIMDS = 1024       # 256 CUs x 4 SIMDs (MI355X_MICROARCH.md chip-level parameters)
+VALU_CYCLES = 4    # wave64 fp64 VALU issue: 16 lanes per clock per SIMD (78.6 TF fp64 vector peak)
+
+
+def find_issue(cfg_key):
+    """VALU instructions per E-step launch and the loaded clock from a committed SQ summary."""
+    best = None
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "**", "sq_*.json"), recursive=True)):
+        try:
+            with open(path) as fh:
+                d = json.load(fh)
+        except Exception:
+            continue
+        for k in d.values():
+            if isinstance(k, dict) and k.get("config_key") == cfg_key and k.get("SQ_INSTS_VALU"):
+                best = {"valu_insts_per_launch": float(k["SQ_INSTS_VALU"]), "clock_ghz": float(k.get("clock_ghz", 2.1)),
+                        "source": os.path.relpath(path, ROOT)}
     return best
 
 
@@ -312,20 +333,24 @@ def main(argv=None):
 
     eng.enqueue_iterations(args.warmup, stats)
     torch.cuda.synchronize()
-    eng.timing(0 if args.no_kernel_timing else args.timing_every)
+    eng.timing(0)
     eng.comm_info(reset=True)
+    # The engine launches on torch's current stream (BaumWelchEngine binds it), so one event pair on
+    # that stream around the whole timed region gives the GPU time per step without perturbing it.
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    ev0.record()
     for _ in range(args.steps):
         eng.enqueue_iterations(1, stats)
+    ev1.record()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    kern_ms, kern_n = eng.timing(0)
-    comm_ranks, ar_ms, ar_n = eng.comm_info(reset=True)
+    gpu_ms_step = ev0.elapsed_time(ev1) / args.steps
     st, _ = eng.status()
     if st.iterations != args.warmup + args.steps:
         raise RuntimeError(f"expected {args.warmup + args.steps} iterations, engine ran {st.iterations}")
@@ -333,6 +358,19 @@ def main(argv=None):
         t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{device}")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    # E-step launches timed one by one (event pairs around each launch serialise the queue, so this
+    # reads ~1-2 us above the undisturbed kernel), in a separate batch after the timed region; plus the
+    # all-reduce per iteration on the engine communicator
+    kern_ms = ar_ms = 0.0
+    kern_n = ar_n = 0
+    comm_ranks = eng.comm_info()[0]
+    if not args.no_kernel_timing:
+        eng.timing(1)
+        eng.comm_info(reset=True)
+        eng.enqueue_iterations(args.timing_batch, stats)
+        torch.cuda.synchronize()
+        kern_ms, kern_n = eng.timing(0)
+        comm_ranks, ar_ms, ar_n = eng.comm_info(reset=True)
 
     synced = None
     if not args.no_synced:
@@ -340,7 +378,15 @@ def main(argv=None):
 
     ms_step = 1000.0 * elapsed / args.steps
     value = R * world * args.steps / elapsed
-    kern_s = kern_ms / max(kern_n, 1) / 1000.0
+    # the kernel time the roofline uses: single rank on the small kernels, every step is ONE launch
+    # (E-step with the merged M-step), so the GPU time per step over the timed region IS the launch
+    # duration (+ the ~1 us dispatch gap between back-to-back launches: conservative); elsewhere (the
+    # wide path's three launches, the all-reduce of N > 1) the per-launch event batch above
+    single_kernel = world == 1 and N <= 16 and not args.deterministic
+    if single_kernel or kern_n == 0:
+        kern_s, kern_src = gpu_ms_step / 1000.0, "HIP events around the timed region / steps (one launch per step)"
+    else:
+        kern_s, kern_src = kern_ms / kern_n / 1000.0, f"HIP events around each of {kern_n} E-step launches after the timed region"
     bu = bytes_per_sequence(T, N)
     wide = N > 16
     cfg_key = f"R{R}_T{T}_N{N}_K{K}_{topo}" + ("_H" if args.symbols == "H" else "")
@@ -351,6 +397,7 @@ def main(argv=None):
         roof = {"bound": "mfma", "achieved": achieved, "peak": FP64_MFMA_PEAK_TFS, "unit": "TFLOP/s",
                 "frac": achieved / FP64_MFMA_PEAK_TFS, "traffic": traffic[0] if traffic else None,
                 "kernel": "k_estep_mfma + k_bnum_gather (E-step)", "kernel_ms": kern_s * 1000.0,
+                "kernel_time_source": kern_src,
                 "flops_per_launch_algorithmic": flops_per_sequence(T, N) * R,
                 "issued_tflops_6N2T": issued, "frac_issued_6N2T": issued / FP64_MFMA_PEAK_TFS,
                 "traffic_source": traffic[1] if traffic else None}
@@ -359,8 +406,22 @@ def main(argv=None):
         roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS, "traffic": traffic[0] if traffic else None,
                 "kernel": "k_estep_small (E-step)", "kernel_ms": kern_s * 1000.0,
+                "kernel_time_source": kern_src,
                 "bytes_per_launch_algorithmic": bu * R,
                 "traffic_source": traffic[1] if traffic else None}
+    # measured-HBM fraction: the PMC bytes per launch (profiles/) over the kernel time -- what the
+    # memory system actually carries (the byte model counts every alpha/beta element once; the
+    # kernel keeps checkpoints, packs and tables on chip)
+    roof["hbm_frac_measured"] = (traffic[0] / kern_s / (HBM_PEAK_GBS * 1e9)) if (traffic and kern_s > 0) else None
+    issue = find_issue(cfg_key)
+    if issue and kern_s > 0 and not wide:  # VALU-issue bound from the committed SQ counters (profiles/)
+        t_issue = issue["valu_insts_per_launch"] * VALU_CYCLES / (SIMDS * issue["clock_ghz"] * 1e9)
+        roof["valu_issue_bound"] = {"t_us": 1e6 * t_issue, "frac": t_issue / kern_s, **issue,
+                                    "model": f"SQ_INSTS_VALU per launch x {VALU_CYCLES} cycles (wave64 fp64 issue) / "
+                                             f"({SIMDS} SIMDs x clock): the time if every SIMD issued VALU "
+                                             "back to back with the work perfectly balanced"}
+    roof["gpu_ms_per_step"] = gpu_ms_step
+    roof["kernel_ms_per_launch_events"] = kern_ms / kern_n if kern_n else None
 
     if rank == 0:
         out = {

@@ -36,8 +36,9 @@ EXPORTED = (
     "hmmbw_get_params", "hmmbw_get_loglik", "hmmbw_score", "hmmbw_timing",
     "hmmbw_set_option", "hmmbw_group_create", "hmmbw_group_destroy", "hmmbw_group_iterate", "hmmbw_group_score",
     "hmmbw_group_timing", "hmmbw_vq_encode", "hmmbw_comm_unique_id", "hmmbw_comm_init",
-    "hmmbw_comm_probe", "hmmbw_comm_info", "hmmbw_comm_payload",
+    "hmmbw_comm_probe", "hmmbw_comm_info", "hmmbw_comm_payload", "hmmbw_iterate_begin", "hmmbw_iterate_end",
 )
+ABI_VERSION = 2
 OPT_SAFE_SCALING = 1
 OPT_ABLATE = 2
 OPT_STAT_COPIES = 3
@@ -84,6 +85,8 @@ def _declare(lib):
         "hmmbw_estep": (ctypes.c_int, [c_ctx, ctypes.c_void_p]),
         "hmmbw_mstep": (ctypes.c_int, [c_ctx, ctypes.c_void_p, ctypes.c_int64]),
         "hmmbw_iterate": (ctypes.c_int, [c_ctx, ctypes.c_int64]),
+        "hmmbw_iterate_begin": (ctypes.c_int, [c_ctx, ctypes.c_int64, P(ctypes.c_void_p), P(ctypes.c_int64)]),
+        "hmmbw_iterate_end": (ctypes.c_int, [c_ctx]),
         "hmmbw_get_status": (ctypes.c_int, [c_ctx, P(Status), ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64]),
         "hmmbw_status_post": (ctypes.c_int, [c_ctx, ctypes.c_int64, P(ctypes.c_int64)]),
         "hmmbw_status_wait": (ctypes.c_int, [c_ctx, ctypes.c_int64, P(Status), ctypes.c_void_p, ctypes.c_int64,
@@ -127,8 +130,9 @@ def lib():
             handle = ctypes.CDLL(LIB_PATH)
             _declare(handle)
             v = handle.hmmbw_abi_version()
-            if v != 1:
-                raise ImportError(f"libhmmbw ABI version {v} != 1")
+            if v != ABI_VERSION:
+                raise ImportError(f"libhmmbw ABI version {v} != {ABI_VERSION} (stale build: rebuild with "
+                                  "`python -m hmm_training_amd.build`)")
             _lib = handle
     return _lib
 

@@ -245,7 +245,14 @@ struct hmmbw_ctx {
     int *d_ebuf = nullptr;
     // native RCCL communicator (hmmbw_comm_init): the multi-rank hmmbw_iterate all-reduces d_ext
     ncclComm_t comm = nullptr;
-    double *d_ext = nullptr;
+    double *d_ext = nullptr;      // non-fused multi-rank paths: the packed statistics to all-reduce
+    long long ext_len = 0;
+    // hmmbw_iterate_begin / _end: one multi-rank iteration split at its all-reduce (the same enqueue
+    // sequence hmmbw_iterate runs around ncclAllReduce); open between the two calls
+    bool ar_open = false;
+    bool ar_fused = false;
+    double *ar_cur = nullptr;
+    long long ar_R = 0;
     // fused native path (small kernels): the E-step accumulates straight into a triple-buffered
     // all-reduce buffer [3][xlen] = {ncopies statistics copies, (max, sum exp) per rank}; the last
     // workgroup of each launch writes the rank's pair (d_ctr: completion counter)
@@ -705,6 +712,7 @@ int hmmbw_set_stream(hmmbw_ctx *c, void *stream) {
 
 int hmmbw_set_rank(hmmbw_ctx *c, int rank, int world) {
     if (!c) return fail(HMMBW_E_INVALID, "null context");
+    if (c->ar_open) return fail(HMMBW_E_STATE, "an iteration is open (hmmbw_iterate_end first)");
     if (world < 1 || rank < 0 || rank >= world) return fail(HMMBW_E_INVALID, "bad rank/world");
     if (int rc = set_device(c)) return rc;
     if (int rc = flush_mstep(c)) return rc;
@@ -736,6 +744,7 @@ int hmmbw_set_observations(hmmbw_ctx *c, const int64_t *offsets, const int32_t *
     if (!c || !offsets || (R > 0 && !symbols && offsets[R] > 0)) return fail(HMMBW_E_INVALID, "null argument");
     if (R < 0) return fail(HMMBW_E_INVALID, "negative sequence count");
     if (offsets[0] != 0) return fail(HMMBW_E_INVALID, "offsets[0] must be 0");
+    if (c->ar_open) return fail(HMMBW_E_STATE, "an iteration is open (hmmbw_iterate_end first)");
     std::vector<int> len((size_t)R);
     for (int64_t r = 0; r < R; ++r) {
         const int64_t T = offsets[r + 1] - offsets[r];
@@ -893,6 +902,7 @@ int hmmbw_set_observations(hmmbw_ctx *c, const int64_t *offsets, const int32_t *
 
 int hmmbw_set_option(hmmbw_ctx *c, int key, int64_t value) {
     if (!c) return fail(HMMBW_E_INVALID, "null context");
+    if (c->ar_open) return fail(HMMBW_E_STATE, "an iteration is open (hmmbw_iterate_end first)");
     if (key == HMMBW_OPT_SAFE_SCALING) {
         c->force_safe = value != 0;
         return HMMBW_OK;
@@ -927,6 +937,7 @@ int hmmbw_set_option(hmmbw_ctx *c, int key, int64_t value) {
 
 int hmmbw_set_params(hmmbw_ctx *c, const double *pi, const double *A, const double *B) {
     if (!c || !pi || !A || !B) return fail(HMMBW_E_INVALID, "null argument");
+    if (c->ar_open) return fail(HMMBW_E_STATE, "an iteration is open (hmmbw_iterate_end first)");
     if (int rc = set_device(c)) return rc;
     if (int rc = flush_mstep(c)) return rc;  // it would overwrite the new parameters later
     HIP_TRY(hipStreamSynchronize(c->stream));
@@ -954,6 +965,7 @@ int hmmbw_set_params(hmmbw_ctx *c, const double *pi, const double *A, const doub
 
 int hmmbw_reset_training(hmmbw_ctx *c, double epsilon, int64_t max_iterations) {
     if (!c) return fail(HMMBW_E_INVALID, "null context");
+    if (c->ar_open) return fail(HMMBW_E_STATE, "an iteration is open (hmmbw_iterate_end first)");
     if (int rc = set_device(c)) return rc;
     if (int rc = flush_mstep(c)) return rc;
     hipLaunchKernelGGL(k_init_state, dim3(1), dim3(1), 0, c->stream, c->state(), epsilon, (long long)max_iterations);
@@ -973,6 +985,7 @@ int hmmbw_stats_len(const hmmbw_ctx *c, int64_t *n) {
 
 int hmmbw_estep(hmmbw_ctx *c, double *stats_dev) {
     if (int rc = check_ready(c, true)) return rc;
+    if (c->ar_open) return fail(HMMBW_E_STATE, "an iteration is open (hmmbw_iterate_end first)");
     if (!stats_dev) return fail(HMMBW_E_INVALID, "null stats buffer");
     if (c->pend.on && !c->can_merge())
         if (int rc = flush_mstep(c)) return rc;
@@ -990,6 +1003,7 @@ int hmmbw_estep(hmmbw_ctx *c, double *stats_dev) {
 
 int hmmbw_mstep(hmmbw_ctx *c, double *stats_dev, int64_t n_seq_global) {
     if (int rc = check_ready(c, true)) return rc;
+    if (c->ar_open) return fail(HMMBW_E_STATE, "an iteration is open (hmmbw_iterate_end first)");
     if (!stats_dev) return fail(HMMBW_E_INVALID, "null stats buffer");
     if (int rc = flush_mstep(c)) return rc;
     hmmbw_ctx::Pending &p = c->pend;
@@ -1005,54 +1019,108 @@ int hmmbw_mstep(hmmbw_ctx *c, double *stats_dev, int64_t n_seq_global) {
     return c->can_merge() ? HMMBW_OK : flush_mstep(c);
 }
 
+// First half of one multi-rank EM iteration: this rank's E-step, leaving in *buf (*len doubles, device
+// memory of the context) the partial statistics that every rank must all-reduce (sum) before mr_end.
+// Small kernels: fused (the E-step accumulates straight into a triple-buffered all-reduce buffer and
+// its last workgroup writes the rank's (max, sum exp) pair; no k_reduce_local launch).  Wide and
+// deterministic paths: hmmbw_estep + k_reduce_local into d_ext.  The layout is rank-independent: every
+// rank all-reduces the same buffer shape, also a rank whose shard is empty.
+static int mr_begin(hmmbw_ctx *c, long long n_seq_global, double **buf, long long *len) {
+    if (c->ar_open) return fail(HMMBW_E_STATE, "an iteration is open (hmmbw_iterate_end first)");
+    const bool fused = !c->wide && !c->det;
+    if (fused) {
+        // rounded to 256 B so all three buffers keep the copies' alignment (a 16-B shift splits the
+        // B-numerator rows' 64-B segments over two cache lines; ~0.7 us per launch at cfg3)
+        const long long xl = ((long long)c->ncopies * c->copy_len() + 2LL * c->world + 31) / 32 * 32;
+        if (c->xlen != xl) {
+            if (int rc = flush_mstep(c)) return rc;
+            HIP_TRY(hipStreamSynchronize(c->stream));
+            dfree(c->d_xbuf);
+            if (int rc = dalloc(&c->d_xbuf, 3 * (size_t)xl)) return rc;
+            HIP_TRY(hipMemsetAsync(c->d_xbuf, 0, sizeof(double) * 3 * (size_t)xl, c->stream));
+            c->xlen = xl;
+            c->e_count = 0;
+        }
+        if (c->pend.on && !c->can_merge())
+            if (int rc = flush_mstep(c)) return rc;
+        const long long e = c->e_count++;
+        double *X = c->d_xbuf + (e % 3) * c->xlen, *Xn = c->d_xbuf + ((e + 1) % 3) * c->xlen;
+        const long long ll_off = (long long)c->ncopies * c->copy_len();
+        // accumulate into X (the merged M-step reads the previous, all-reduced X), clear the next
+        if (c->nblocks > 0) {
+            if (int rc = launch_estep(c, false, c->state(), X, c->llpart(e), Xn, c->xlen, true,
+                                      X + ll_off + 2LL * c->rank))
+                return rc;
+        } else {  // empty shard: contribute zeros (no E-step launch clears the buffers)
+            HIP_TRY(hipMemsetAsync(X, 0, sizeof(double) * (size_t)c->xlen, c->stream));
+        }
+        *buf = X;
+        *len = c->xlen;
+    } else {
+        if (c->ext_len != c->stats_len()) {  // sized by the world of hmmbw_set_rank
+            if (int rc = flush_mstep(c)) return rc;
+            HIP_TRY(hipStreamSynchronize(c->stream));
+            dfree(c->d_ext);
+            if (int rc = dalloc(&c->d_ext, (size_t)c->stats_len())) return rc;
+            HIP_TRY(hipMemsetAsync(c->d_ext, 0, sizeof(double) * (size_t)c->stats_len(), c->stream));
+            c->ext_len = c->stats_len();
+        }
+        if (int rc = hmmbw_estep(c, c->d_ext)) return rc;
+        *buf = c->d_ext;
+        *len = c->ext_len;
+    }
+    c->ar_open = true;
+    c->ar_fused = fused;
+    c->ar_cur = *buf;
+    c->ar_R = n_seq_global;
+    return HMMBW_OK;
+}
+
+// Second half: the M-step from the all-reduced buffer (merged into the next E-step launch when it can).
+static int mr_end(hmmbw_ctx *c) {
+    if (!c->ar_open) return fail(HMMBW_E_STATE, "no open iteration (hmmbw_iterate_begin first)");
+    c->ar_open = false;
+    if (!c->ar_fused) return hmmbw_mstep(c, c->ar_cur, c->ar_R);
+    hmmbw_ctx::Pending &p = c->pend;
+    p.on = true;
+    p.local = false;
+    p.src = c->ar_cur;
+    p.nsrc = c->ncopies;
+    p.ll = c->ar_cur + (long long)c->ncopies * c->copy_len();
+    p.nll = c->world;
+    p.ext = c->ar_cur;
+    p.R = c->ar_R;
+    return c->can_merge() ? HMMBW_OK : flush_mstep(c);
+}
+
+int hmmbw_iterate_begin(hmmbw_ctx *c, int64_t n_seq_global, double **buf, int64_t *n_doubles) {
+    if (int rc = check_ready(c, true)) return rc;
+    if (!buf || !n_doubles) return fail(HMMBW_E_INVALID, "null argument");
+    if (n_seq_global < 0) return fail(HMMBW_E_INVALID, "negative sequence count");
+    long long len = 0;
+    if (int rc = mr_begin(c, n_seq_global, buf, &len)) return rc;
+    *n_doubles = len;
+    return HMMBW_OK;
+}
+
+int hmmbw_iterate_end(hmmbw_ctx *c) {
+    if (int rc = check_ready(c, true)) return rc;
+    return mr_end(c);
+}
+
 int hmmbw_iterate(hmmbw_ctx *c, int64_t n_iter) {
     if (int rc = check_ready(c, true)) return rc;
+    if (c->ar_open) return fail(HMMBW_E_STATE, "an iteration is open (hmmbw_iterate_end first)");
     if (c->world != 1 || c->comm) {
         // multi-rank with the native communicator: estep -> ncclAllReduce (this stream) -> mstep
         if (!c->comm) return fail(HMMBW_E_STATE, "multi-rank hmmbw_iterate needs hmmbw_comm_init "
-                                                 "(or use estep / all-reduce / mstep)");
+                                                 "(or use hmmbw_iterate_begin / all-reduce / _end)");
         Rccl *r = nullptr;
         if (int rc = rccl_load(nullptr, &r)) return rc;
-        // small kernels: fused (no k_reduce_local launch); the wide path keeps estep + k_reduce_local
-        // (rank-independent: every rank must all-reduce the same buffer layout, also a rank whose
-        // shard is empty)
-        const bool fused = !c->wide && !c->det;
-        if (fused) {
-            // rounded to 256 B so all three buffers keep the copies' alignment (a 16-B shift splits the
-            // B-numerator rows' 64-B segments over two cache lines; ~0.7 us per launch at cfg3)
-            const long long xl = ((long long)c->ncopies * c->copy_len() + 2LL * c->world + 31) / 32 * 32;
-            if (c->xlen != xl) {
-                if (int rc = flush_mstep(c)) return rc;
-                HIP_TRY(hipStreamSynchronize(c->stream));
-                dfree(c->d_xbuf);
-                if (int rc = dalloc(&c->d_xbuf, 3 * (size_t)xl)) return rc;
-                HIP_TRY(hipMemsetAsync(c->d_xbuf, 0, sizeof(double) * 3 * (size_t)xl, c->stream));
-                c->xlen = xl;
-                c->e_count = 0;
-            }
-        }
         for (int64_t i = 0; i < n_iter; ++i) {
-            double *ar = c->d_ext;
-            size_t ar_len = (size_t)c->stats_len();
-            if (fused) {
-                if (c->pend.on && !c->can_merge())
-                    if (int rc = flush_mstep(c)) return rc;
-                const long long e = c->e_count++;
-                double *X = c->d_xbuf + (e % 3) * c->xlen, *Xn = c->d_xbuf + ((e + 1) % 3) * c->xlen;
-                const long long ll_off = (long long)c->ncopies * c->copy_len();
-                // accumulate into X (the merged M-step reads the previous, all-reduced X), clear the next
-                if (c->nblocks > 0) {
-                    if (int rc = launch_estep(c, false, c->state(), X, c->llpart(e), Xn, c->xlen, true,
-                                              X + ll_off + 2LL * c->rank))
-                        return rc;
-                } else {  // empty shard: contribute zeros (no E-step launch clears the buffers)
-                    HIP_TRY(hipMemsetAsync(X, 0, sizeof(double) * (size_t)c->xlen, c->stream));
-                }
-                ar = X;
-                ar_len = (size_t)c->xlen;
-            } else if (int rc = hmmbw_estep(c, c->d_ext)) {
-                return rc;
-            }
+            double *ar = nullptr;
+            long long ar_len = 0;
+            if (int rc = mr_begin(c, c->R_global, &ar, &ar_len)) return rc;
             hipEvent_t e0 = nullptr, e1 = nullptr;
             if (c->timing && (c->ar_seq++ % c->timing) == 0) {
                 if (int rc = take_events(c->ar_free, &e0, &e1)) return rc;
@@ -1060,9 +1128,12 @@ int hmmbw_iterate(hmmbw_ctx *c, int64_t n_iter) {
             }
             // also at world 1 (RCCL's in-place 1-rank sum is a copy kernel, ~2 us): the 1-rank
             // communicator tests then exercise the same ncclAllReduce call as an 8-GPU run
-            c->ar_len_last = (long long)ar_len;
-            ncclResult_t e = r->all_reduce(ar, ar, ar_len, ncclFloat64, ncclSum, c->comm, c->stream);
-            if (e != ncclSuccess) return rccl_fail(r, e, "ncclAllReduce");
+            c->ar_len_last = ar_len;
+            ncclResult_t e = r->all_reduce(ar, ar, (size_t)ar_len, ncclFloat64, ncclSum, c->comm, c->stream);
+            if (e != ncclSuccess) {
+                c->ar_open = false;
+                return rccl_fail(r, e, "ncclAllReduce");
+            }
             if (e1) {
                 HIP_TRY(hipEventRecord(e1, c->stream));
                 c->ar_pending.push_back(e0);
@@ -1070,21 +1141,7 @@ int hmmbw_iterate(hmmbw_ctx *c, int64_t n_iter) {
                 if (c->ar_pending.size() >= 256)
                     if (int rc = drain_pairs(c->ar_pending, c->ar_free, &c->ar_ms, &c->ar_n)) return rc;
             }
-            if (fused) {
-                hmmbw_ctx::Pending &p = c->pend;
-                p.on = true;
-                p.local = false;
-                p.src = ar;
-                p.nsrc = c->ncopies;
-                p.ll = ar + (long long)c->ncopies * c->copy_len();
-                p.nll = c->world;
-                p.ext = ar;
-                p.R = c->R_global;
-                if (!c->can_merge())
-                    if (int rc = flush_mstep(c)) return rc;
-            } else if (int rc = hmmbw_mstep(c, c->d_ext, c->R_global)) {
-                return rc;
-            }
+            if (int rc = mr_end(c)) return rc;
         }
         return HMMBW_OK;
     }
@@ -1183,7 +1240,8 @@ int hmmbw_status_wait(hmmbw_ctx *c, int64_t ticket, hmmbw_status *st, hmmbw_iter
     const IterState h = *sn.st;
     fill_status(h, st);
     if (rec && count > 0) {
-        if (first < sn.first || first + count > h.iteration || first + count > sn.first + kHist)
+        if (first < sn.first || first + count > h.iteration || first + count > sn.first + kHist ||
+            first < h.iteration - kHist)  // overwritten in the ring before the snapshot was taken
             return fail(HMMBW_E_INVALID, "requested iteration records are not in this snapshot");
         for (int64_t i = 0; i < count; ++i) {
             const int64_t k = first + i - sn.first;
@@ -1405,6 +1463,7 @@ int hmmbw_comm_init(hmmbw_ctx *c, const char *rccl_path, const void *id, int ran
         return rc;
     }
     HIP_TRY(hipMemset(c->d_ext, 0, sizeof(double) * (size_t)c->stats_len()));
+    c->ext_len = c->stats_len();
     c->comm = comm;
     c->R_global = n_seq_global;
     return HMMBW_OK;

@@ -1122,6 +1122,21 @@ __device__ bool record_iteration(const MArgs &m, const IterState &in, double L) 
     return cont;
 }
 
+// L = LSE_r log P_r (:503) from one all-reduced (max, sum exp) pair per rank, by ONE thread in rank
+// order.  Every multi-rank M-step variant (the merged prologue, k_mstep, k_mstep_grid) forms L with
+// this function, so ranks that run different variants (an empty shard cannot merge its M-step) still
+// hold bitwise-identical L and diff and take the same stop decision (:346).
+__device__ __forceinline__ double lse_rank_pairs(const double *ll, long long n) {
+    double mx = -INFINITY;
+    for (long long r = 0; r < n; ++r)
+        if (ll[2 * r + 1] > 0.0) mx = fmax(mx, ll[2 * r]);
+    double s = 0.0;
+    if (mx != -INFINITY)
+        for (long long r = 0; r < n; ++r)
+            if (ll[2 * r + 1] > 0.0) s += ll[2 * r + 1] * exp(ll[2 * r] - mx);
+    return (s > 0.0) ? mx + log(s) : -INFINITY;
+}
+
 // M-step kernels entered after convergence carry the state over to the next slot and do nothing else
 __device__ __forceinline__ bool carry_if_done(const MArgs &m) {
     if (!m.state->done) return false;
@@ -1143,15 +1158,7 @@ __device__ void mstep_block(const MArgs &m) {
         combine_ll_pairs<ATOMIC>(m.llpart, m.nblocks, sh, &mx, &s);
         if (tid == 0) sL = (s > 0.0) ? mx + log(s) : -INFINITY;
     } else if (tid == 0) {
-        const double *ll = m.llpart;  // one (max, sum exp) pair per rank, all-reduced
-        double mx = -INFINITY;
-        for (long long r = 0; r < m.nblocks; ++r)
-            if (ll[2 * r + 1] > 0.0) mx = fmax(mx, ll[2 * r]);
-        double s = 0.0;
-        if (mx != -INFINITY)
-            for (long long r = 0; r < m.nblocks; ++r)
-                if (ll[2 * r + 1] > 0.0) s += ll[2 * r + 1] * exp(ll[2 * r] - mx);
-        sL = (s > 0.0) ? mx + log(s) : -INFINITY;
+        sL = lse_rank_pairs(m.llpart, m.nblocks);  // one (max, sum exp) pair per rank, all-reduced
         for (long long r = 0; r < 2 * m.nblocks; ++r) m.zero_ll[r] = 0.0;
     }
     const int N = m.N, K = m.K;
@@ -1221,15 +1228,7 @@ __device__ void mstep_grid(const MArgs &m) {
         combine_ll_pairs<false>(m.llpart, m.nblocks, sh, &mx, &s);
         if (tid == 0) sL = (s > 0.0) ? mx + log(s) : -INFINITY;
     } else if (tid == 0) {
-        const double *ll = m.llpart;  // one (max, sum exp) pair per rank, all-reduced
-        double mx = -INFINITY;
-        for (long long r = 0; r < m.nblocks; ++r)
-            if (ll[2 * r + 1] > 0.0) mx = fmax(mx, ll[2 * r]);
-        double s = 0.0;
-        if (mx != -INFINITY)
-            for (long long r = 0; r < m.nblocks; ++r)
-                if (ll[2 * r + 1] > 0.0) s += ll[2 * r + 1] * exp(ll[2 * r] - mx);
-        sL = (s > 0.0) ? mx + log(s) : -INFINITY;
+        sL = lse_rank_pairs(m.llpart, m.nblocks);  // one (max, sum exp) pair per rank, all-reduced
     }
     for (int i = tid; i < N; i += blockDim.x) {
         const double pn = peek(m, i);
@@ -1404,6 +1403,7 @@ __device__ bool merged_mstep(const EArgs &a, double *sP, double *sH, double *sPA
     constexpr int PB = 2;                   // log-likelihood pairs per thread per pass
     __shared__ double sSm[NSM];
     __shared__ double sMx[NW], sSum[NW];
+    __shared__ double sLr;  // multi-rank: L from the per-rank pairs (lse_rank_pairs)
     __shared__ IterState sIn;
     const MArgs &m = a.m;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -1462,7 +1462,11 @@ __device__ bool merged_mstep(const EArgs &a, double *sP, double *sH, double *sPA
         const int idx = q * BLK + tid;
         if (idx < NSM) sSm[idx] = (idx < len) ? v[q] : 0.0;
     }
-    if (tid == 0) sIn = in;
+    if (tid == 0) {
+        sIn = in;
+        // multi-rank: the same fixed-order fold as the standalone M-step kernels of other ranks
+        if (!m.local_lse) sLr = lse_rank_pairs(m.llpart, nb);
+    }
     __syncthreads();
     PHASE(6);
     if (sIn.done) {  // converged before this launch: device-side no-op
@@ -1553,7 +1557,7 @@ __device__ bool merged_mstep(const EArgs &a, double *sP, double *sH, double *sPA
     double S = 0.0;
 #pragma unroll
     for (int w = 0; w < NW; ++w) S += sSum[w];
-    const double L = (S > 0.0) ? Mb + log(S) : -INFINITY;
+    const double L = m.local_lse ? ((S > 0.0) ? Mb + log(S) : -INFINITY) : sLr;
     const double diff = (sIn.prev_L != -INFINITY) ? fabs(L - sIn.prev_L) : INFINITY;  // :505-508
     const bool cont = (diff >= sIn.epsilon) && (sIn.iteration + 1 < sIn.max_iterations);  // :346
     if (w0) {

@@ -144,6 +144,7 @@ class BaumWelchEngine:
         if native_comm is None:
             native_comm = os.environ.get("HMMBW_NATIVE_COMM", "1") != "0"
         self._want_native = bool(native_comm) and self.world_size > 1
+        self._timing_mode = 0  # hmmbw_timing mode last set through timing()
 
     # -------------------------------------------------------------------------------- set-up
     def set_observations(self, observations: Sequence[np.ndarray] = None, offsets: np.ndarray = None,
@@ -236,6 +237,20 @@ class BaumWelchEngine:
             dist.all_reduce(stats, group=group)  # ONE RCCL all-reduce of the packed fp64 statistics
             check(self._lib.hmmbw_mstep(self._ctx, ptr, self.n_seq_global))
 
+    def iterate_begin(self, n_seq_global: Optional[int] = None) -> Tuple[int, int]:
+        """First half of one multi-rank EM iteration (hmmbw_iterate_begin): enqueue this rank's E-step
+        and return (device pointer, doubles) of the buffer every rank must all-reduce (sum, in place)
+        before iterate_end().  The same enqueue sequence hmmbw_iterate runs around ncclAllReduce."""
+        ptr = ctypes.c_void_p()
+        n = ctypes.c_int64()
+        R = self.n_seq_global if n_seq_global is None else int(n_seq_global)
+        check(self._lib.hmmbw_iterate_begin(self._ctx, R, ctypes.byref(ptr), ctypes.byref(n)))
+        return int(ptr.value or 0), int(n.value)
+
+    def iterate_end(self) -> None:
+        """Second half: the M-step + convergence step from the all-reduced buffer (hmmbw_iterate_end)."""
+        check(self._lib.hmmbw_iterate_end(self._ctx))
+
     def make_stats_buffer(self) -> torch.Tensor:
         return torch.zeros(self.stats_len, dtype=torch.float64, device=f"cuda:{self.device}")
 
@@ -249,9 +264,14 @@ class BaumWelchEngine:
         stats = self.make_stats_buffer() if self.world_size > 1 and not self._native else None
         mpath = metrics if metrics is not None else os.environ.get("HMMBW_METRICS")
         mfh = open(mpath, "a") if (mpath and self.rank == 0) else None
+        timing_prev = self._timing_mode
         if mfh is not None:
-            self.timing(1)
-            self.comm_info(reset=True)
+            # metrics need the E-step kernel time: events around every launch unless the caller already
+            # samples (then its mode and accumulation are left alone; rows use deltas).  Events on every
+            # launch serialise the queue around them, so ms_per_iter reads a few us high in this mode.
+            if timing_prev == 0:
+                self.timing(1)
+            self._mbase = (*self.timing(-1), *self.comm_info()[1:])
         # Pipelined: chunk k + 1 is queued before chunk k's status snapshot is read (hmmbw_status_post
         # / _wait wait for the snapshot only), so the device never idles on a host round trip.  The
         # snapshots lag one iteration (the last iteration's M-step is merged into the next launch);
@@ -300,7 +320,8 @@ class BaumWelchEngine:
                     self._write_metrics(mfh, reported, recs, time.perf_counter() - t_last, new)
         finally:
             if mfh is not None:
-                self.timing(0)
+                if timing_prev == 0:
+                    self.timing(0)
                 mfh.close()
         return st
 
@@ -321,8 +342,11 @@ class BaumWelchEngine:
         wall time per enqueued iteration (incl. the host status sync), utterances/s/iter over all ranks,
         the mean E-step kernel time (HIP events), the SURVEY §8(d) byte model over it as GB/s and as a
         fraction of the 8 TB/s HBM peak, and the mean RCCL all-reduce time (engine communicator)."""
-        k_ms, k_n = self.timing(1)
-        _, ar_ms, ar_n = self.comm_info(reset=True)
+        k_ms1, k_n1 = self.timing(-1)  # query only: deltas since the previous row
+        _, ar_ms1, ar_n1 = self.comm_info()
+        k_ms0, k_n0, ar_ms0, ar_n0 = self._mbase
+        self._mbase = (k_ms1, k_n1, ar_ms1, ar_n1)
+        k_ms, k_n, ar_ms, ar_n = k_ms1 - k_ms0, k_n1 - k_n0, ar_ms1 - ar_ms0, ar_n1 - ar_n0
         estep_s = k_ms / k_n / 1e3 if k_n else None
         nbytes = 24 * self.n_symbols_total + 16 * self.N * self.n_symbols_total + 8 * self.n_seq
         per_iter = wall_s / max(enqueued, 1)
@@ -357,6 +381,10 @@ class BaumWelchEngine:
         return out[: self.n_seq]
 
     def timing(self, enable: int = -1) -> Tuple[float, int]:
+        """(accumulated E-step ms, timed launches) of hmmbw_timing; enable >= 0 also resets and sets the
+        mode (0 off, k: every k-th launch), enable < 0 only queries."""
+        if enable >= 0:
+            self._timing_mode = int(enable)
         ms = ctypes.c_double()
         n = ctypes.c_int64()
         check(self._lib.hmmbw_timing(self._ctx, int(enable), ctypes.byref(ms), ctypes.byref(n)))

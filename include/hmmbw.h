@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define HMMBW_ABI_VERSION 1
+#define HMMBW_ABI_VERSION 2 /* 2: hmmbw_iterate_begin/_end, status snapshots, comm info/payload */
 
 #define HMMBW_OK 0
 #define HMMBW_E_INVALID (-1)        /* bad argument (shape, range, null pointer)             */
@@ -135,6 +135,20 @@ int hmmbw_comm_info(hmmbw_ctx *ctx, int *n_ranks, double *total_ms, int64_t *cou
  * before the first): the fused small path all-reduces its statistics copies plus one (max, sum exp)
  * pair per rank, 256-B aligned; the other paths the packed statistics (hmmbw_stats_len). */
 int hmmbw_comm_payload(const hmmbw_ctx *ctx, int64_t *n_doubles);
+
+/* One multi-rank EM iteration split at its all-reduce, for callers that bring their own collective
+ * (torch.distributed, MPI, an in-process sum over several contexts) or test the exact enqueue
+ * sequence an RCCL run makes without RCCL: hmmbw_iterate_begin enqueues this rank's E-step (on the
+ * small kernels the fused one that accumulates straight into the all-reduce buffer and writes the
+ * rank's (max, sum exp) pair of log P; elsewhere hmmbw_estep into the packed statistics) and returns
+ * the DEVICE buffer *buf of *n_doubles doubles that the caller must all-reduce (sum, in place, ordered
+ * after the context's stream) before hmmbw_iterate_end, which enqueues the M-step + convergence step
+ * (hmm_training.py:415-514; merged into the next E-step launch when it can).  n_seq_global is the R of
+ * :424.  The buffer layout does not depend on the shard, so every rank (an empty shard too) passes the
+ * same length.  hmmbw_iterate on a context with hmmbw_comm_init runs exactly begin -> ncclAllReduce ->
+ * end per iteration.  Any other training call between the two returns HMMBW_E_STATE. */
+int hmmbw_iterate_begin(hmmbw_ctx *ctx, int64_t n_seq_global, double **buf, int64_t *n_doubles);
+int hmmbw_iterate_end(hmmbw_ctx *ctx);
 
 /* SYNC. Status plus the iteration records [first, first+count) (ring of 4096 entries). */
 int hmmbw_get_status(hmmbw_ctx *ctx, hmmbw_status *status, hmmbw_iter_record *records, int64_t first,

@@ -1,22 +1,24 @@
-"""Full-size BASELINE configurations on the GPU (cfg3, cfg4 shard and whole, cfg5 shard), several EM
-iterations each, through the production path (hmmbw_iterate: E-step with the merged M-step).
+"""Full-size BASELINE configurations on the GPU, compared with the oracle on the SAME inputs.
 
-At these sizes the oracle cannot replay whole runs in seconds, so parity rests on size-independent
-properties, all from hmm_training.py:351-514:
-  * EM monotonicity: sum_r log P_r never decreases from one iteration to the next (Baum-Welch is an
-    EM algorithm for the product of the sequence likelihoods; the reference's convergence scalar
-    L = LSE_r log P_r is recorded too and must be finite);
-  * E-step sum rules on a fresh statistics pass with the final parameters:
-    sum_k B_num[j, k] = gamma_den_all[j], sum_j xi[i, j] = gamma_den_excl[i],
-    sum_i pi_num[i] = number of sequences with finite log P, sum_j gamma_den_all[j] = sum_r T_r;
-  * the M-step the kernels apply to those statistics equals the reference's formulas evaluated on
-    the host from the same statistics (:415-497, incl. the 1e-20 floor), to 1e-12;
-  * returned (A, B, pi) rows sum to 1 (:524-541);
-  * 48 sampled sequences' log P against oracle.forward_loglik (hmm_testing.py:49-104 = the E-step's
-    alpha recursion) at rtol 1e-9, and the per-workgroup LSE pairs against the oracle's LSE.
+Each case runs the production path (hmmbw_iterate: E-step launches with the merged M-step) for several
+EM iterations and checks against oracle.hmm_training (hmm_training.py:351-514, run with OpenMP over
+utterances on the host's cores: the same log-domain terms as the serial restatement, merged per thread):
+  * every recorded L (:503) at rtol 1e-9, every sequence's log P of the last E-step at rtol 1e-9;
+  * the returned (pi, A, B) (:524-541) and the working parameters (exp of the reference's log_pi /
+    log_a / log_b) at the north-star tolerance |x - ref| <= 1e-6 |ref| + 1e-15;
+then one statistics pass (hmmbw_estep) with the final parameters against oracle.estep_logstats:
+  * the COMPLETE packed statistics (pi_num, xi, gamma_den_excl, gamma_den_all, B_num) at rtol 1e-9,
+    every log P at rtol 1e-9 and the rank's (max, sum exp) pair against the oracle's LSE;
+  * the M-step the kernels apply to them (hmmbw_mstep) against the reference's formulas (:415-497),
+    and the sum rules (sum_k B_num = gamma_den_all, sum_j xi = gamma_den_excl, sum pi_num = R,
+    sum gamma_den_all = R T).
+Configurations: cfg3 (10,000 x 200, N=8, K=256) left-to-right and dense, the cfg4 per-GPU shard
+(12,500 x 200) on skewed 'H' symbols, cfg4 whole (100,000 x 200) on one GPU (one iteration), a
+full-shape cfg5 slice (512 x 400, N=64, K=1024, dense) and the cfg5 per-GPU shard (6,250 x 400) against
+the oracle, and the whole cfg5 set (50,000 x 400) on one GPU by sum rules and 64 sampled log P (the
+oracle would need minutes per iteration there).
 """
 import ctypes
-import os
 import sys
 
 import numpy as np
@@ -25,6 +27,8 @@ import pytest
 from conftest import ROOT
 
 pytestmark = pytest.mark.gpu
+
+PARAM_RTOL, PARAM_ATOL, LL_RTOL, STAT_RTOL = 1e-6, 1e-15, 1e-9, 1e-9
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -50,6 +54,12 @@ def _params(N, K, topology, seed):
     return pi, A, B
 
 
+def assert_params(mine, ref, what):
+    mine, ref = np.asarray(mine), np.asarray(ref)
+    err = np.abs(mine - ref) - (PARAM_RTOL * np.abs(ref) + PARAM_ATOL)
+    assert np.all(err <= 0), f"{what}: worst excess {err.max():.3e} at {np.unravel_index(np.argmax(err), err.shape)}"
+
+
 def host_mstep(g, R):
     """The reference's M-step (hmm_training.py:415-497) in the linear domain, from packed statistics."""
     pi = np.where(g["pi_num"] > 0, g["pi_num"] / R, 0.0)
@@ -61,87 +71,138 @@ def host_mstep(g, R):
     return pi, A, B
 
 
-def run_fullsize(oracle, R, T, N, K, topology, iters, seed, symbols="U"):
-    import torch
-    from hmm_training_amd._lib import check
-    from hmm_training_amd.engine import BaumWelchEngine, StatsLayout
-    sym = _symbols(R, T, N, K, symbols, seed)
-    off = np.arange(R + 1, dtype=np.int64) * T
-    pi, A, B = _params(N, K, topology, seed)
-    with BaumWelchEngine(N, K, topology=topology) as eng:
-        eng.set_observations(offsets=off, symbols=sym)
-        eng.set_params(pi, A, B)
-        assert eng.topology == topology
-        # -------- several production iterations (hmmbw_iterate), one at a time --------
-        eng.reset(0.0, iters)
-        sums = []
-        for k in range(iters):
-            eng.enqueue_iterations(1)
-            st, recs = eng.status(k, 1)
-            assert st.iterations == k + 1
-            lp = eng.loglik()  # log P_r under the parameters that entered iteration k
-            assert np.all(np.isfinite(lp)), f"iteration {k}: non-finite log P"
-            assert np.isfinite(recs[0][0])
-            assert np.isclose(recs[0][0], oracle.lse(lp), rtol=1e-12)  # L = LSE_r log P_r (:503)
-            sums.append(float(np.sum(lp)))
-        assert st.done and not st.converged
-        for a, b in zip(sums, sums[1:]):
-            assert b >= a - 1e-9 * abs(a), f"EM decreased sum log P: {a} -> {b}"
-        p_out, A_out, B_out = eng.params(normalise=True)
-        for m in (A_out, B_out):
-            np.testing.assert_allclose(m.sum(1), 1.0, rtol=1e-12)
-        assert np.isclose(p_out.sum(), 1.0, rtol=1e-12)
-        p_cur, A_cur, B_cur = eng.params(normalise=False)
-        # -------- a statistics pass with the current parameters: sum rules + M-step --------
-        eng.reset(0.0, 1)
-        stats = eng.make_stats_buffer()
-        check(eng._lib.hmmbw_estep(eng._ctx, ctypes.c_void_p(stats.data_ptr())))
-        torch.cuda.synchronize()
-        g = StatsLayout(N, K).decode(stats.cpu().numpy())
-        ll = eng.loglik()
-        check(eng._lib.hmmbw_mstep(eng._ctx, ctypes.c_void_p(stats.data_ptr()), R))
-        p_m, A_m, B_m = eng.params(normalise=False)
-    assert np.all(np.isfinite(ll))
+def assert_stats(g, s, R, T):
+    """Packed device statistics vs the oracle's log-domain ones (exp), plus the sum rules."""
+    with np.errstate(under="ignore"):
+        for key, lkey in (("pi_num", "log_pi_num"), ("xi", "log_xi"), ("gamma_den_excl", "log_gden_excl"),
+                          ("gamma_den_all", "log_gden_all"), ("B_num", "log_bnum")):
+            ref = np.exp(getattr(s, lkey))
+            np.testing.assert_allclose(g[key], ref, rtol=STAT_RTOL, atol=1e-300, err_msg=key)
     np.testing.assert_allclose(g["B_num"].sum(1), g["gamma_den_all"], rtol=1e-11)
     np.testing.assert_allclose(g["xi"].sum(1), g["gamma_den_excl"], rtol=1e-11)
     assert np.isclose(g["pi_num"].sum(), R, rtol=1e-12)
     assert np.isclose(g["gamma_den_all"].sum(), R * T, rtol=1e-12)
-    assert np.isclose(g["gamma_den_excl"].sum(), R * (T - 1), rtol=1e-12)
+
+
+def statistics_pass(eng, N, K, R):
+    """One hmmbw_estep with the current parameters; returns (decoded stats, log P, M-step params)."""
+    import torch
+    from hmm_training_amd._lib import check
+    from hmm_training_amd.engine import StatsLayout
+    eng.reset(0.0, 1)
+    stats = eng.make_stats_buffer()
+    check(eng._lib.hmmbw_estep(eng._ctx, ctypes.c_void_p(stats.data_ptr())))
+    torch.cuda.synchronize()
+    g = StatsLayout(N, K).decode(stats.cpu().numpy())
+    ll = eng.loglik()
+    check(eng._lib.hmmbw_mstep(eng._ctx, ctypes.c_void_p(stats.data_ptr()), R))
+    return g, ll, eng.params(normalise=False)
+
+
+def run_vs_oracle(oracle, R, T, N, K, topology, iters, seed, symbols="U"):
+    from hmm_training_amd.engine import BaumWelchEngine, StatsLayout
+    sym = _symbols(R, T, N, K, symbols, seed)
+    off = np.arange(R + 1, dtype=np.int64) * T
+    sym64 = sym.astype(np.int64)
+    pi, A, B = _params(N, K, topology, seed)
+    ref = oracle.hmm_training(off, sym64, N, K, 0.0, iters, pi, A, B)
+    assert ref.iterations == iters
+    with BaumWelchEngine(N, K, topology=topology) as eng:
+        eng.set_observations(offsets=off, symbols=sym)
+        eng.set_params(pi, A, B)
+        assert eng.topology == topology
+        # -------- production iterations, enqueued together (merged M-steps) --------
+        eng.reset(0.0, iters)
+        eng.enqueue_iterations(iters)
+        st, recs = eng.status(0, iters)
+        assert st.iterations == iters and st.done and not st.converged
+        np.testing.assert_allclose([L for L, _ in recs], ref.trace_L, rtol=LL_RTOL)
+        np.testing.assert_allclose(eng.loglik(), ref.logP, rtol=LL_RTOL)  # E-step of the last iteration
+        p_out, A_out, B_out = eng.params(normalise=True)
+        assert_params(A_out, ref.A, "A")
+        assert_params(B_out, ref.B, "B")
+        assert_params(p_out, ref.pi, "pi")
+        p_cur, A_cur, B_cur = eng.params(normalise=False)
+        with np.errstate(under="ignore"):
+            assert_params(p_cur, np.exp(ref.log_pi), "log_pi")
+            assert_params(A_cur, np.exp(ref.log_A), "log_A")
+            assert_params(B_cur, np.exp(ref.log_B), "log_B")
+        # -------- statistics pass with the final parameters --------
+        g, ll, (p_m, A_m, B_m) = statistics_pass(eng, N, K, R)
+    s = oracle.estep_logstats(off, sym64, N, K, p_cur, A_cur, B_cur)
+    np.testing.assert_allclose(ll, s.logP, rtol=LL_RTOL)
+    assert_stats(g, s, R, T)
+    assert np.isclose(StatsLayout.lse_of_pairs(g["ll_pairs"]), oracle.lse(s.logP), rtol=1e-12)
     hp, hA, hB = host_mstep(g, R)
     np.testing.assert_allclose(p_m, hp, rtol=1e-12, atol=1e-300)
     np.testing.assert_allclose(A_m, hA, rtol=1e-12, atol=1e-300)
     np.testing.assert_allclose(B_m, hB, rtol=1e-12, atol=1e-300)
-    rng = np.random.default_rng(seed + 1)
-    pick = np.sort(rng.choice(R, size=48, replace=False))
-    ref = oracle.forward_loglik(np.arange(len(pick) + 1) * T, sym.reshape(R, T)[pick].reshape(-1).astype(np.int64),
-                                N, K, p_cur, A_cur, B_cur)
-    np.testing.assert_allclose(ll[pick], ref, rtol=1e-9)
-    from hmm_training_amd.engine import StatsLayout as SL
-    assert np.isclose(SL.lse_of_pairs(g["ll_pairs"]), oracle.lse(ll), rtol=1e-12)
-    return sums
 
 
-def test_cfg3_full_size_multi_iteration(oracle):
-    """BASELINE cfg3: 10,000 x T=200, N=8, K=256, left-to-right, 4 EM iterations."""
-    run_fullsize(oracle, 10_000, 200, 8, 256, "left_to_right", 4, seed=3)
+def test_cfg3_full_size_vs_oracle(oracle_mt):
+    """BASELINE cfg3: 10,000 x T=200, N=8, K=256, left-to-right (the headline kernel), 4 EM iterations."""
+    run_vs_oracle(oracle_mt, 10_000, 200, 8, 256, "left_to_right", 4, seed=3)
 
 
-def test_cfg3_full_size_dense(oracle):
-    run_fullsize(oracle, 10_000, 200, 8, 256, "dense", 3, seed=33)
+def test_cfg3_full_size_dense_vs_oracle(oracle_mt):
+    run_vs_oracle(oracle_mt, 10_000, 200, 8, 256, "dense", 3, seed=33)
 
 
-def test_cfg4_shard_full_size(oracle):
+def test_cfg4_shard_full_size_vs_oracle(oracle_mt):
     """BASELINE cfg4's per-GPU shard: 12,500 x T=200, N=8, K=256, 3 EM iterations, skewed symbols
     (hot symbols contend in the B-numerator histogram)."""
-    run_fullsize(oracle, 12_500, 200, 8, 256, "left_to_right", 3, seed=4, symbols="H")
+    run_vs_oracle(oracle_mt, 12_500, 200, 8, 256, "left_to_right", 3, seed=4, symbols="H")
 
 
-def test_cfg4_whole_on_one_gpu(oracle):
-    """BASELINE cfg4 unsharded: 100,000 x T=200, N=8, K=256 on one GPU (fits HBM), 3 EM iterations."""
-    run_fullsize(oracle, 100_000, 200, 8, 256, "left_to_right", 3, seed=44)
+def test_cfg4_whole_on_one_gpu_vs_oracle(oracle_mt):
+    """BASELINE cfg4 unsharded: 100,000 x T=200, N=8, K=256 on one GPU, one EM iteration + statistics."""
+    run_vs_oracle(oracle_mt, 100_000, 200, 8, 256, "left_to_right", 1, seed=44)
 
 
-def test_cfg5_shard_full_size(oracle):
-    """BASELINE cfg5's per-GPU shard: 6,250 x T=400, N=64, K=1024, dense A (the fp64-MFMA wide path,
-    k_estep_mfma + k_bnum_gather + k_mstep_grid), 2 EM iterations."""
-    run_fullsize(oracle, 6_250, 400, 64, 1024, "dense", 2, seed=5)
+def test_cfg5_full_shape_slice_vs_oracle(oracle_mt):
+    """BASELINE cfg5's shape (T=400, N=64, K=1024, dense: the fp64-MFMA wide path, k_estep_mfma +
+    k_bnum_gather + k_mstep_grid) on 512 sequences, 2 EM iterations, everything against the oracle."""
+    run_vs_oracle(oracle_mt, 512, 400, 64, 1024, "dense", 2, seed=55)
+
+
+def test_cfg5_shard_full_size_vs_oracle(oracle_mt):
+    """BASELINE cfg5's per-GPU shard: 6,250 x T=400, N=64, K=1024, dense, 2 EM iterations vs the oracle."""
+    run_vs_oracle(oracle_mt, 6_250, 400, 64, 1024, "dense", 2, seed=5)
+
+
+def test_cfg5_whole_on_one_gpu(oracle_mt):
+    """BASELINE cfg5 unsharded: 50,000 x T=400, N=64, K=1024, dense on ONE GPU (20 GB of alpha_hat and
+    gamma rows; the reference's per-utterance xi allocation, hmm_training.py:328-339, cannot run it), 2 EM
+    iterations: the L trace against the per-sequence log P, sum rules, the M-step against the reference
+    formulas, and 64 sampled sequences' log P against oracle.forward_loglik (hmm_testing.py:49-104)."""
+    from hmm_training_amd.engine import BaumWelchEngine, StatsLayout
+    oracle = oracle_mt
+    R, T, N, K = 50_000, 400, 64, 1024
+    sym = _symbols(R, T, N, K, "U", 5)
+    off = np.arange(R + 1, dtype=np.int64) * T
+    pi, A, B = _params(N, K, "dense", 5)
+    with BaumWelchEngine(N, K, topology="dense") as eng:
+        eng.set_observations(offsets=off, symbols=sym)
+        eng.set_params(pi, A, B)
+        eng.reset(0.0, 2)
+        eng.enqueue_iterations(2)
+        st, recs = eng.status(0, 2)
+        assert st.iterations == 2
+        lp = eng.loglik()
+        assert np.all(np.isfinite(lp))
+        assert np.isclose(recs[-1][0], oracle.lse(lp), rtol=1e-12)
+        p_cur, A_cur, B_cur = eng.params(normalise=False)
+        g, ll, (p_m, A_m, B_m) = statistics_pass(eng, N, K, R)
+    np.testing.assert_allclose(g["B_num"].sum(1), g["gamma_den_all"], rtol=1e-11)
+    np.testing.assert_allclose(g["xi"].sum(1), g["gamma_den_excl"], rtol=1e-11)
+    assert np.isclose(g["pi_num"].sum(), R, rtol=1e-12)
+    assert np.isclose(g["gamma_den_all"].sum(), R * T, rtol=1e-12)
+    hp, hA, hB = host_mstep(g, R)
+    np.testing.assert_allclose(p_m, hp, rtol=1e-12, atol=1e-300)
+    np.testing.assert_allclose(A_m, hA, rtol=1e-12, atol=1e-300)
+    np.testing.assert_allclose(B_m, hB, rtol=1e-12, atol=1e-300)
+    pick = np.sort(np.random.default_rng(6).choice(R, size=64, replace=False))
+    ref = oracle.forward_loglik(np.arange(len(pick) + 1) * T, sym.reshape(R, T)[pick].reshape(-1).astype(np.int64),
+                                N, K, p_cur, A_cur, B_cur)
+    np.testing.assert_allclose(ll[pick], ref, rtol=LL_RTOL)
+    assert np.isclose(StatsLayout.lse_of_pairs(g["ll_pairs"]), oracle.lse(ll), rtol=1e-12)

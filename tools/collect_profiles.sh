@@ -20,7 +20,8 @@ for W in lr_cfg3 lrH_cfg3 dense_cfg3 cfg5; do
     --write "profiles/$DEST/pmc_WRITE_SIZE_$W.csv" \
     --calib-fetch "profiles/$DEST/pmc_calib_FETCH_SIZE.csv" --calib-write "profiles/$DEST/pmc_calib_WRITE_SIZE.csv" \
     --kernel "${KER[$W]}" --config-key "${KEY[$W]}" --out "profiles/$DEST/traffic_$W.json"
-  python3 tools/pmc_summary.py "profiles/$DEST/pmc_SQ_$W.csv" "${KER[$W]}" > "profiles/$DEST/sq_$W.json"
+  python3 tools/pmc_summary.py "profiles/$DEST/pmc_SQ_$W.csv" "${KER[$W]}" --config-key "${KEY[$W]}" \
+    --kernel-stats "profiles/$DEST/kernel_stats_$W.csv" > "profiles/$DEST/sq_$W.json"
 done
 for W in cfg2 vq; do
   cp "$SRC/trace_$W/run_kernel_stats.csv" "profiles/$DEST/kernel_stats_$W.csv"

@@ -3,7 +3,11 @@ tools/pmc_sq.sh output directory), as JSON, with the derived LDS bank-conflict r
 (SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE: extra cycles / all LDS-array cycles, MI355X_MICROARCH.md §LDS)
 and VALU / LDS instructions per wave.
 
-    python tools/pmc_summary.py <csv or dir> <kernel substring[,substring...]>
+    python tools/pmc_summary.py <csv or dir> <kernel substring[,substring...]> [--config-key KEY]
+        [--kernel-stats run_kernel_stats.csv]
+
+With GRBM_GUI_ACTIVE in the pass and the kernel's mean duration from a kernel-trace stats CSV of the same
+workload, also the loaded clock (GRBM_GUI_ACTIVE / 8 XCDs / duration, MI355X_MICROARCH.md DVFS note).
 """
 import collections
 import csv
@@ -13,7 +17,12 @@ import os
 import sys
 
 
-def main(src, kernels):
+def mean_ns(stats_csv, kern):
+    rows = [r for r in csv.DictReader(open(stats_csv)) if kern in r["Name"]]
+    return sum(float(r["AverageNs"]) for r in rows) / len(rows) if rows else None
+
+
+def main(src, kernels, config_key=None, kernel_stats=None):
     files = [src] if os.path.isfile(src) else glob.glob(f"{src}/p*/run_counter_collection.csv")
     out = {}
     for kern in kernels.split(","):
@@ -30,9 +39,23 @@ def main(src, kernels):
                 if c in d:
                     d[c.lower() + "_per_wave"] = d[c] / d["SQ_WAVES"]
         d["dispatches"] = max((len(v) for v in vals.values()), default=0)
+        if config_key:
+            d["config_key"] = config_key
+        if kernel_stats and d.get("GRBM_GUI_ACTIVE"):
+            ns = mean_ns(kernel_stats, kern)
+            if ns:
+                d["kernel_ns_trace"] = ns
+                d["clock_ghz"] = d["GRBM_GUI_ACTIVE"] / 8.0 / ns
         out[kern] = d
     print(json.dumps(out, indent=2))
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2])
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("src")
+    ap.add_argument("kernels")
+    ap.add_argument("--config-key")
+    ap.add_argument("--kernel-stats")
+    a = ap.parse_args()
+    main(a.src, a.kernels, a.config_key, a.kernel_stats)

@@ -17,7 +17,7 @@ for C in FETCH_SIZE WRITE_SIZE; do
   step calib $C
   timeout -k 10 120 rocprofv3 --pmc $C --output-format csv -d "$OUT/calib_$C" -o run -- "$OUT/pmc_calib" > "$OUT/calib_$C.log" 2>&1 || exit 1
 done
-SQ="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_BUSY_CYCLES SQ_WAVE_CYCLES"
+SQ="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE"
 declare -A ARGS=(
   [lr_cfg3]="--steps 20 --warmup 3 --no-cpu-baseline --no-synced"
   [lrH_cfg3]="--steps 20 --warmup 3 --no-cpu-baseline --no-synced --symbols H"
