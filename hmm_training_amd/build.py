@@ -42,11 +42,13 @@ def _jobs():
     return max(1, min(16, os.cpu_count() or 1))
 
 
-def build(force: bool = False, verbose: bool = False, defines=(), out: str = OUT, tag: str = "release") -> str:
-    """Compile every unit (in parallel) and link `out`; skipped when `out` is newer than all sources."""
+def build(force: bool = False, verbose: bool = False, defines=(), out: str = OUT, tag: str = "release",
+          only=None) -> str:
+    """Compile every unit (in parallel) and link `out`; skipped when `out` is newer than all sources.
+    only: object stems to recompile (development: the other units' existing objects are relinked)."""
     sources = [HDR] + glob.glob(os.path.join(CSRC, "*"))
     stamp = max(os.path.getmtime(p) for p in sources)
-    if not force and os.path.exists(out) and os.path.getmtime(out) >= stamp:
+    if not force and only is None and os.path.exists(out) and os.path.getmtime(out) >= stamp:
         return out
     objdir = os.path.join(PKG, "_obj", tag)
     os.makedirs(objdir, exist_ok=True)
@@ -54,6 +56,9 @@ def build(force: bool = False, verbose: bool = False, defines=(), out: str = OUT
     for src, extra, stem in units():
         obj = os.path.join(objdir, stem + ".o")
         cmds.append((obj, [HIPCC, *FLAGS, *defines, *extra, "-c", src, "-o", obj]))
+    links = [o for o, _ in cmds]
+    if only is not None:
+        cmds = [(o, c) for o, c in cmds if os.path.basename(o)[:-2] in set(only) or not os.path.exists(o)]
 
     def run(cmd):
         if verbose:
@@ -68,11 +73,12 @@ def build(force: bool = False, verbose: bool = False, defines=(), out: str = OUT
     cmds.sort(key=lambda x: ("small_n" not in x[0], -int(x[0].rsplit("_n", 1)[-1][:-2]) if "small_n" in x[0] else 0))
     with cf.ThreadPoolExecutor(max_workers=_jobs()) as ex:
         list(ex.map(run, [c for _, c in cmds]))
-    link = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *[o for o, _ in cmds], "-o", out + ".tmp"]
+    link = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *links, "-o", out + ".tmp"]
     run(link)
     os.replace(out + ".tmp", out)
     return out
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose=True))
+    only = [a.split("=", 1)[1] for a in sys.argv if a.startswith("--only=")]
+    print(build(force="--force" in sys.argv, verbose=True, only=only[0].split(",") if only else None))

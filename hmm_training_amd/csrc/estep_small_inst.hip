@@ -36,7 +36,7 @@ extern "C" {
 int hmmbw_debug_phase_times(unsigned long long *out, int64_t nwaves) {
     if (!out || nwaves < 0 || nwaves > kPhaseWaves) return -1;
     if (hipDeviceSynchronize() != hipSuccess) return -2;
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase), sizeof(unsigned long long) * 8 * nwaves) != hipSuccess)
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase), sizeof(unsigned long long) * kPhaseSlots * nwaves) != hipSuccess)
         return -2;
     return 0;
 }

@@ -23,11 +23,18 @@ namespace hmmbw {
 // the small E-step's phases, read back with hmmbw_debug_phase_times.
 #ifdef HMMBW_PHASE_TIMES
 constexpr int kPhaseWaves = 1 << 16;
-static __device__ unsigned long long g_phase[kPhaseWaves][8];
+constexpr int kPhaseSlots = 16;
+static __device__ unsigned long long g_phase[kPhaseWaves][kPhaseSlots];
 #define PHASE(k)                                                                               \
     do {                                                                                       \
         const long long w_ = (long long)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);   \
         if ((threadIdx.x & 63) == 0 && w_ < kPhaseWaves) g_phase[w_][k] = wall_clock64();      \
+    } while (0)
+// diagnostics: wait for every outstanding memory operation of the wave, then stamp
+#define PHASE_DRAIN(k)                   \
+    do {                                 \
+        __builtin_amdgcn_s_waitcnt(0);   \
+        PHASE(k);                        \
     } while (0)
 // shader-clock stamp at the start of forward (d = 0) / backward (d = 1) chunk c (c < 64); only with
 // -DHMMBW_CHUNK_TIMES too: its conditional stores inside the sweeps change their s_waitcnt placement
@@ -49,6 +56,9 @@ static __device__ unsigned long long g_chunk[4096][2][64];
     } while (0)
 #define PHASE(k) \
     do {         \
+    } while (0)
+#define PHASE_DRAIN(k) \
+    do {               \
     } while (0)
 #endif
 
@@ -373,6 +383,7 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
     if constexpr (!FWD_ONLY)  // clear the next iteration's statistics (single rank: triple buffer)
         for (long long i = bid * blockDim.x + tid; i < a.zero_len; i += nblk * blockDim.x)
             a.zero[i] = 0.0;
+    PHASE(13);
     const int j = lane & (G - 1), u = lane / G;
     const int K = a.K;
     double *sP = smem;                   // LDSTAB: P-table [K][GP] {x, y} (see kHistOff)
@@ -928,6 +939,7 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
             if (x != 0.0) unsafeAtomicAdd(&accb[a.off_bnum + (long long)k * N + jj], x);
         }
     }
+    PHASE(11);
     // per-block (max, sum exp) of log P for the convergence scalar
     block_ll_partial(logp_lane, ll_valid, sRed, a.llpart + 2 * bid);
     PHASE(4);
@@ -1409,6 +1421,7 @@ __device__ bool merged_mstep(const EArgs &a, double *sP, double *sH, double *sPA
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int K = a.K;
     const long long len = m.copy_len;
+    PHASE(8);
     // ---- every load issued before any use: statistics, log-likelihood pairs, convergence state ----
     double v[SB];
 #pragma unroll
@@ -1446,6 +1459,7 @@ __device__ bool merged_mstep(const EArgs &a, double *sP, double *sH, double *sPA
         in.last_L = m.state->last_L;
         in.last_diff = m.state->last_diff;
     }
+    PHASE_DRAIN(9);
     // ---- L = LSE_r log P_r (:503) in two passes: max, then sum of exp(m - max) ----
     double mx = -INFINITY;
 #pragma unroll
@@ -1545,6 +1559,7 @@ __device__ bool merged_mstep(const EArgs &a, double *sP, double *sH, double *sPA
             }
         }
     }
+    PHASE(10);
     // zero the pad columns [N, GP) of every row (products, histogram, b)
     if constexpr (GP > N) {
         for (int i = tid; i < K * (GP - N); i += BLK) {

@@ -21,7 +21,7 @@ sys.path.insert(0, ROOT)
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--R", type=int, default=10000)
+    ap.add_argument("--R", default="10000", help="comma-separated sequence counts")
     ap.add_argument("--T", type=int, default=200)
     ap.add_argument("--N", type=int, default=8)
     ap.add_argument("--K", type=int, default=256)
@@ -39,7 +39,13 @@ def main():
     import torch
     from hmm_training_amd.engine import BaumWelchEngine
     from hmm_training_amd.hmm_training import default_initial_params
-    R, T, N, K = a.R, a.T, a.N, a.K
+    for R in [int(x) for x in a.R.split(",")]:
+        run_one(a, R, torch, BaumWelchEngine, default_initial_params, out_dir)
+
+
+def run_one(a, R, torch, BaumWelchEngine, default_initial_params, out_dir):
+    print(f"==== R={R}")
+    T, N, K = a.T, a.N, a.K
     rng = np.random.default_rng(3)
     sym = rng.integers(0, K, size=R * T).astype(np.int32)
     pi, A, Bm = default_initial_params(N, K)
@@ -54,7 +60,7 @@ def main():
     U = 64 // (1 << max(1, (N - 1).bit_length()))
     nw = (R + U - 1) // U
     nw_pad = ((nw + 3) // 4) * 4
-    buf = np.zeros((nw_pad, 8), dtype=np.uint64)
+    buf = np.zeros((nw_pad, 16), dtype=np.uint64)
     l = eng._lib
     l.hmmbw_debug_phase_times.argtypes = [ctypes.c_void_p, ctypes.c_int64]
     rc = l.hmmbw_debug_phase_times(buf.ctypes.data, nw_pad)
@@ -71,7 +77,8 @@ def main():
         r = us(t[:, k] - t0)
         print(f"at {names[k]:<8s} rel-start  min {r.min():7.2f}  p50 {np.median(r):7.2f}  max {r.max():7.2f} us")
     if np.all(t[:, 6] > 0):  # merged M-step prologue: statistics gathered / tables built
-        for k, nm in ((6, "mstep-loads"), (7, "mstep-tables")):
+        for k, nm in ((13, "zero-cleared"), (8, "mstep-entry"), (9, "stats-landed"), (6, "mstep-loads"),
+                      (7, "mstep-sum"), (10, "tables-written"), (11, "hist-flushed")):
             r = us(t[:, k] - t0)
             print(f"at {nm:<12s} rel-start  min {r.min():7.2f}  p50 {np.median(r):7.2f}  max {r.max():7.2f} us")
     np.save(os.path.join(out_dir, "phase_nomerge.npy" if a.no_merge else "phase_merge.npy"), t)
