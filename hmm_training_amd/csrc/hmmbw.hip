@@ -31,6 +31,8 @@
 //   k_mstep_grid    large N x K (wide path): B re-estimated by the whole grid, the rest by workgroup 0.
 //   k_finalise  the reference's return-path normalisation (:524-541).
 #include <dlfcn.h>
+
+#include <cstdlib>
 #include <rccl/rccl.h>
 
 #include "hmmbw_device.hpp"
@@ -233,6 +235,8 @@ struct hmmbw_ctx {
     // observations
     long long R = 0, nwaves = 0;
     long long nblocks = 0;
+    long long nfull = 0;          // small kernels: workgroups with 4 active waves (then xact-wave ones)
+    int xact = 4;
     uint16_t *d_sym = nullptr;
     long long *d_wsym = nullptr, *d_wckoff = nullptr, *d_wspoff = nullptr;
     int *d_wT = nullptr, *d_wfull = nullptr, *d_slen = nullptr, *d_sseq = nullptr;
@@ -346,6 +350,8 @@ EArgs make_eargs(hmmbw_ctx *c) {
     a.off_gex = c->off_gex();
     a.off_gall = c->off_gall();
     a.off_bnum = c->off_bnum();
+    a.nfull = c->nfull;
+    a.xact = c->xact;
     return a;
 }
 
@@ -815,7 +821,30 @@ int hmmbw_set_observations(hmmbw_ctx *c, const int64_t *offsets, const int32_t *
         }
     free_obs(c);
     const int wpb = kBlock / kWave;
-    const long long nblocks = c->wide ? nwaves : (nwaves + wpb - 1) / wpb;  // wide: one tile per block
+    long long nblocks = c->wide ? nwaves : (nwaves + wpb - 1) / wpb;  // wide: one tile per block
+    // Small kernels, more waves than SIMDs: one full 4-wave workgroup per CU, then the remaining waves
+    // in workgroups of xact = 2 active waves (one per CU while they fit), so the SIMDs that must run a
+    // second wave are spread over twice as many CUs, which then share their LDS and memory pipes among
+    // 6 waves instead of 8.  cfg3 (1,250 waves): 38.2 -> 36.5 us per iteration; xact = 1 (a prologue
+    // and histogram flush per extra wave) and 3 measured no better.  HMMBW_XACT
+    // overrides it (diagnostics: 1..4, 4 = every workgroup full).
+    long long nfull = nblocks;
+    int xact = wpb;
+    if (!c->wide && !c->det) {
+        int ncu = 0;
+        (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device);
+        if (ncu > 0 && nwaves > (long long)ncu * wpb) {
+            const long long extra = nwaves - (long long)ncu * wpb;
+            const char *xe = std::getenv("HMMBW_XACT");
+            int xa = extra <= 2LL * ncu ? 2 : wpb;
+            if (xe) xa = std::max(1, std::min(wpb, std::atoi(xe)));
+            if (xa < wpb && (extra + xa - 1) / xa <= ncu) {
+                nfull = ncu;
+                xact = xa;
+                nblocks = nfull + (extra + xa - 1) / xa;
+            }
+        }
+    }
     int rc = dalloc(&c->d_sym, (size_t)std::max(symtot, 1LL));
     if (!rc) rc = dalloc(&c->d_wsym, (size_t)nwaves);
     if (!rc) rc = dalloc(&c->d_wckoff, (size_t)nwaves);
@@ -896,6 +925,8 @@ int hmmbw_set_observations(hmmbw_ctx *c, const int64_t *offsets, const int32_t *
     c->R = R;
     c->nwaves = nwaves;
     c->nblocks = nblocks;
+    c->nfull = nfull;
+    c->xact = xact;
     c->has_obs = true;
     return HMMBW_OK;
 }

@@ -145,6 +145,10 @@ struct EArgs {
     int *done_ctr;     // ... and the workgroup completion counter that picks the workgroup forming it
     MArgs m;
     long long off_S, off_gex, off_gall, off_bnum;
+    // wave -> workgroup map of the small kernels: workgroups [0, nfull) run 4 sequence-group waves each,
+    // the workgroups after them only xact (the waves beyond one per SIMD spread over more CUs)
+    long long nfull;
+    int xact;
 };
 
 // Grouped launch (k_estep_small_group): per-model arguments and first workgroups (start[nm] = grid)
@@ -436,7 +440,10 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
     }
     PHASE(1);
 
-    const long long wave = bid * (blockDim.x >> 6) + wv;
+    const int wpb = blockDim.x >> 6;
+    const bool xblk = bid >= a.nfull;
+    const long long wave = xblk ? a.nfull * wpb + (bid - a.nfull) * a.xact + wv : bid * wpb + wv;
+    const bool wactive = !xblk || wv < a.xact;
     double *accb = a.copies + (bid % a.ncopies) * a.copy_len;
     double S[NS];
 #pragma unroll
@@ -445,7 +452,7 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
     double logp_lane = -INFINITY;
     bool ll_valid = false;
 
-    if (wave < a.L.nwaves) {
+    if (wactive && wave < a.L.nwaves) {
         const long long slot = wave * U + u;
         const int T = a.L.slot_len[slot];
         const int seq = a.L.slot_seq[slot];

@@ -206,3 +206,40 @@ def test_cfg5_whole_on_one_gpu(oracle_mt):
                                 N, K, p_cur, A_cur, B_cur)
     np.testing.assert_allclose(ll[pick], ref, rtol=LL_RTOL)
     assert np.isclose(StatsLayout.lse_of_pairs(g["ll_pairs"]), oracle.lse(ll), rtol=1e-12)
+
+
+@pytest.mark.parametrize("xact", [None, "1", "3"])
+def test_spread_extra_waves_ragged_vs_oracle(oracle_mt, monkeypatch, xact):
+    """More waves than SIMDs (9,000 ragged sequences = 1,125 waves on 1,024 SIMDs): one full workgroup
+    per CU, then workgroups of xact active waves (default 2; HMMBW_XACT forces 1 or 3), with inactive
+    waves in them; every statistic and the trained model against the oracle (hmm_training.py:351-514)."""
+    from hmm_training_amd.engine import BaumWelchEngine, StatsLayout, to_csr
+    if xact is not None:
+        monkeypatch.setenv("HMMBW_XACT", xact)
+    rng = np.random.default_rng(9)
+    R, N, K, iters = 9000, 8, 256, 3
+    obs = [rng.integers(0, K, size=int(t)) for t in rng.integers(60, 160, size=R)]
+    off, sym = to_csr(obs)
+    pi, A, B = _params(N, K, "left_to_right", 9)
+    ref = oracle_mt.hmm_training(off, sym.astype(np.int64), N, K, 0.0, iters, pi, A, B)
+    with BaumWelchEngine(N, K, topology="left_to_right") as eng:
+        eng.set_observations(obs)
+        eng.set_params(pi, A, B)
+        eng.reset(0.0, iters)
+        eng.enqueue_iterations(iters)
+        st, recs = eng.status(0, iters)
+        np.testing.assert_allclose([L for L, _ in recs], ref.trace_L, rtol=LL_RTOL)
+        np.testing.assert_allclose(eng.loglik(), ref.logP, rtol=LL_RTOL)
+        p_out, A_out, B_out = eng.params(normalise=True)
+        p_cur, A_cur, B_cur = eng.params(normalise=False)
+        g, ll, _ = statistics_pass(eng, N, K, R)
+    assert_params(A_out, ref.A, "A")
+    assert_params(B_out, ref.B, "B")
+    assert_params(p_out, ref.pi, "pi")
+    s = oracle_mt.estep_logstats(off, sym.astype(np.int64), N, K, p_cur, A_cur, B_cur)
+    np.testing.assert_allclose(ll, s.logP, rtol=LL_RTOL)
+    with np.errstate(under="ignore"):
+        for key, lkey in (("pi_num", "log_pi_num"), ("xi", "log_xi"), ("gamma_den_excl", "log_gden_excl"),
+                          ("gamma_den_all", "log_gden_all"), ("B_num", "log_bnum")):
+            np.testing.assert_allclose(g[key], np.exp(getattr(s, lkey)), rtol=STAT_RTOL, atol=1e-300, err_msg=key)
+    assert np.isclose(StatsLayout.lse_of_pairs(g["ll_pairs"]), oracle_mt.lse(s.logP), rtol=1e-12)

@@ -18,7 +18,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--R", type=int, default=10000)
-    ap.add_argument("--modes", default="single,multirank,native")
+    ap.add_argument("--modes", default="single,multirank,native,split")
+    ap.add_argument("--copies", type=int, default=None, help="statistics copies (default: the library's)")
     a = ap.parse_args()
     import torch
     import torch.distributed as dist
@@ -35,7 +36,7 @@ def main():
     pi, A, B = default_initial_params(N, K)
     out = {}
     for mode in a.modes.split(","):
-        eng = BaumWelchEngine(N, K, device=0, rank=0, world_size=1)
+        eng = BaumWelchEngine(N, K, device=0, rank=0, world_size=1, stat_copies=a.copies)
         eng.set_observations(offsets=off, symbols=sym)
         eng.set_params(pi, A, B)
         eng.reset(0.0, 10 ** 9)
@@ -56,6 +57,11 @@ def main():
             if mode in ("single", "native"):
                 eng.enqueue_iterations(n)
                 return
+            if mode == "split":  # the fused multi-rank kernels with no collective (world 1: identity)
+                for _ in range(n):
+                    eng.iterate_begin(R)
+                    eng.iterate_end()
+                return
             for _ in range(n):
                 eng._lib.hmmbw_estep(eng._ctx, ptr)
                 dist.all_reduce(stats)
@@ -67,9 +73,10 @@ def main():
         t_host = time.perf_counter() - t0
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
-        out[mode] = {"us_per_iter": 1e6 * dt / a.steps, "host_enqueue_us_per_iter": 1e6 * t_host / a.steps}
+        out[mode] = {"us_per_iter": 1e6 * dt / a.steps, "host_enqueue_us_per_iter": 1e6 * t_host / a.steps,
+                     "payload_bytes": eng.comm_payload_bytes() if mode == "native" else None}
         eng.close()
-    print(json.dumps(out), flush=True)
+    print(json.dumps({"R": R, "copies": a.copies, **out}), flush=True)
     dist.destroy_process_group()
 
 
