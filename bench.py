@@ -173,6 +173,7 @@ def find_traffic(cfg_key):
 
 SIMDS = 1024       # 256 CUs x 4 SIMDs (MI355X_MICROARCH.md chip-level parameters)
 VALU_CYCLES = 4    # wave64 fp64 VALU issue: 16 lanes per clock per SIMD (78.6 TF fp64 vector peak)
+CLOCK_MAX_GHZ = 2.4  # MI355X max shader clock: the issue bound at the peak clock is the optimistic one
 
 
 def find_issue(cfg_key):
@@ -186,8 +187,10 @@ def find_issue(cfg_key):
             continue
         for k in d.values():
             if isinstance(k, dict) and k.get("config_key") == cfg_key and k.get("SQ_INSTS_VALU"):
-                best = {"valu_insts_per_launch": float(k["SQ_INSTS_VALU"]), "clock_ghz": float(k.get("clock_ghz", 2.1)),
-                        "source": os.path.relpath(path, ROOT)}
+                # GRBM_GUI_ACTIVE / 8 / kernel time reads high on dispatches under ~0.3 ms
+                # (MI355X_MICROARCH.md, DVFS give-back), so the bound is priced at the max clock
+                best = {"valu_insts_per_launch": float(k["SQ_INSTS_VALU"]), "clock_ghz": CLOCK_MAX_GHZ,
+                        "clock_ghz_grbm_estimate": k.get("clock_ghz"), "source": os.path.relpath(path, ROOT)}
     return best
 
 

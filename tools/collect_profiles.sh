@@ -8,10 +8,11 @@ mkdir -p "profiles/$DEST"
 cp "$SRC/calib_FETCH_SIZE/run_counter_collection.csv" "profiles/$DEST/pmc_calib_FETCH_SIZE.csv"
 cp "$SRC/calib_WRITE_SIZE/run_counter_collection.csv" "profiles/$DEST/pmc_calib_WRITE_SIZE.csv"
 declare -A KEY=([lr_cfg3]=R10000_T200_N8_K256_left_to_right [lrH_cfg3]=R10000_T200_N8_K256_left_to_right_H
-                [dense_cfg3]=R10000_T200_N8_K256_dense [cfg5]=R6250_T400_N64_K1024_dense)
+                [dense_cfg3]=R10000_T200_N8_K256_dense [cfg5]=R6250_T400_N64_K1024_dense
+                [cfg4shard]=R12500_T200_N8_K256_left_to_right)
 declare -A KER=([lr_cfg3]=k_estep_small [lrH_cfg3]=k_estep_small [dense_cfg3]=k_estep_small
-                [cfg5]="k_estep_mfma,k_bnum_gather")
-for W in lr_cfg3 lrH_cfg3 dense_cfg3 cfg5; do
+                [cfg5]="k_estep_mfma,k_bnum_gather" [cfg4shard]=k_estep_small)
+for W in lr_cfg3 lrH_cfg3 dense_cfg3 cfg5 cfg4shard; do
   cp "$SRC/trace_$W/run_kernel_stats.csv" "profiles/$DEST/kernel_stats_$W.csv"
   for C in FETCH_SIZE WRITE_SIZE SQ; do
     cp "$SRC/pmc_${C}_$W/run_counter_collection.csv" "profiles/$DEST/pmc_${C}_$W.csv"
@@ -31,5 +32,6 @@ grep -h '"metric"' "$SRC/bench_dense.log" > "profiles/$DEST/bench_dense_cfg3.jso
 grep -h '"metric"' "$SRC/bench_H.log" > "profiles/$DEST/bench_lrH_cfg3.json"
 grep -h '"metric"' "$SRC/bench_cfg5.log" > "profiles/$DEST/bench_cfg5.json"
 grep -h '"metric"' "$SRC/bench_cfg4shard.log" > "profiles/$DEST/bench_cfg4shard.json"
+grep -h '"metric"' "$SRC/bench_cfg5_50k.log" > "profiles/$DEST/bench_cfg5_50k.json"
 grep -h '"workload"' "$SRC/bench_cfg2_full.log" > "profiles/$DEST/bench_cfg2_grouped.json"
 grep -h '"kernel"' "$SRC/bench_vq.log" > "profiles/$DEST/bench_vq.json"

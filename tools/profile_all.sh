@@ -23,8 +23,9 @@ declare -A ARGS=(
   [lrH_cfg3]="--steps 20 --warmup 3 --no-cpu-baseline --no-synced --symbols H"
   [dense_cfg3]="--steps 20 --warmup 3 --no-cpu-baseline --no-synced --topology dense"
   [cfg5]="--steps 5 --warmup 2 --no-cpu-baseline --no-synced --workload cfg5"
+  [cfg4shard]="--steps 20 --warmup 3 --no-cpu-baseline --no-synced --workload cfg4"
 )
-for W in lr_cfg3 lrH_cfg3 dense_cfg3 cfg5; do
+for W in lr_cfg3 lrH_cfg3 dense_cfg3 cfg5 cfg4shard; do
   BENCH="$R/bench.py ${ARGS[$W]}"
   step trace $W
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace_$W" -o run -- python3 $BENCH > "$OUT/bench_trace_$W.log" 2>&1 || exit 1
@@ -45,5 +46,6 @@ timeout -k 10 300 python3 "$R/bench.py" --topology dense --no-cpu-baseline > "$O
 timeout -k 10 300 python3 "$R/bench.py" --symbols H --no-cpu-baseline > "$OUT/bench_H.log" 2>&1 || exit 1
 timeout -k 10 300 python3 "$R/bench.py" --workload cfg5 --steps 10 --warmup 2 --no-cpu-baseline > "$OUT/bench_cfg5.log" 2>&1 || exit 1
 timeout -k 10 300 python3 "$R/bench.py" --workload cfg4 --no-cpu-baseline > "$OUT/bench_cfg4shard.log" 2>&1 || exit 1
+timeout -k 10 300 python3 "$R/bench.py" --workload cfg5 --R 50000 --steps 5 --warmup 1 --no-cpu-baseline --no-synced > "$OUT/bench_cfg5_50k.log" 2>&1 || exit 1
 timeout -k 10 300 python3 "$R/tools/bench_cfg2.py" > "$OUT/bench_cfg2_full.log" 2>&1 || exit 1
 step done
