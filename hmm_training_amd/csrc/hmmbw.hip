@@ -241,6 +241,8 @@ struct hmmbw_ctx {
     long long *d_wsym = nullptr, *d_wckoff = nullptr, *d_wspoff = nullptr;
     int *d_wT = nullptr, *d_wfull = nullptr, *d_slen = nullptr, *d_sseq = nullptr;
     double *d_ck = nullptr, *d_logp = nullptr, *d_llpart = nullptr;  // llpart: [2][nblocks][2]
+    long long cktot = 0;          // checkpoint doubles of the layout
+    double *d_zf = nullptr;       // dense small kernels: every z_t, kChunk x cktot (allocated on first use)
     // wide path: gamma rows per position and the symbol -> rows index of k_bnum_gather
     double *d_gam = nullptr;
     long long *d_bptr = nullptr;
@@ -309,7 +311,7 @@ int set_device(hmmbw_ctx *c) {
 void free_obs(hmmbw_ctx *c) {
     dfree(c->d_sym); dfree(c->d_wsym); dfree(c->d_wckoff); dfree(c->d_wspoff);
     dfree(c->d_wT); dfree(c->d_wfull); dfree(c->d_slen); dfree(c->d_sseq);
-    dfree(c->d_ck); dfree(c->d_sp); dfree(c->d_ebuf); dfree(c->d_logp); dfree(c->d_llpart);
+    dfree(c->d_ck); dfree(c->d_sp); dfree(c->d_ebuf); dfree(c->d_logp); dfree(c->d_llpart); dfree(c->d_zf);
     dfree(c->d_gam); dfree(c->d_bptr); dfree(c->d_brows); dfree(c->d_part);
     c->has_obs = false;
 }
@@ -465,6 +467,11 @@ int plan_estep(hmmbw_ctx *c, bool fwd_only, const IterState *state, double *copi
             const int NV = (lr ? 2 : c->N) + 3;
             const size_t tabs = c->lds_table_doubles();
             p.lds = sizeof(double) * (tabs + (size_t)wpb * c->G * NV + 8);
+            if (HMMBW_ZFULL && !lr && !fwd_only) {  // dense: the forward stores every z_t (hmmbw_device.hpp)
+                if (!c->d_zf)
+                    if (int rc = dalloc(&c->d_zf, (size_t)std::max(c->cktot * kChunk, 1LL))) return rc;
+                a.ckpt = c->d_zf;
+            }
         }
     }
     if (p.grid > 0 && merge && !fwd_only && c->pend.on && c->can_merge()) {
@@ -854,6 +861,7 @@ int hmmbw_set_observations(hmmbw_ctx *c, const int64_t *offsets, const int32_t *
     if (!rc) rc = dalloc(&c->d_slen, (size_t)(nwaves * U));
     if (!rc) rc = dalloc(&c->d_sseq, (size_t)(nwaves * U));
     if (!rc) rc = dalloc(&c->d_ck, (size_t)std::max(cktot, 1LL));
+    c->cktot = cktot;
     if (!rc) {
         if (c->wide) rc = dalloc(&c->d_ebuf, (size_t)std::max(sptot, 1LL));
         else rc = dalloc(&c->d_sp, (size_t)std::max(sptot, 1LL));

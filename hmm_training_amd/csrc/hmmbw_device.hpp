@@ -257,6 +257,19 @@ __device__ __forceinline__ void bcast_dot(double &acc0, double &acc1, double z, 
     });
 }
 
+// Dense xi partial sums of a G = 8 wave (lane = 8 u + j) on the 4x4x4 f64 MFMA: its block is lane
+// bits 2-3, A lane 16k + 4blk + m holds A[m][k], B lane 16k + 4blk + n holds B[k][n], D lane
+// 16m + 4blk + n holds D[m][n] (tools/ubench_mfma4.hip, profiles/r3/ubench_mfma4x4x4.txt).  With
+// z as A and v as B, block (j >> 2, u & 1) sums over the seqs u >> 1:
+//   X[0] lane 16m + 4jh + 8u0 + n:  sum z_t(4jh + m) v_{t+1}(4jh + n)            (diagonal 4x4 blocks)
+//   X[1] with v row_half_mirrored (state j -> 7 - j):  ... v_{t+1}(4(1 - jh) + 3 - n)  (off-diagonal)
+// The accumulation is off the forward/backward chains, so the MFMA's ~44-cycle SrcC latency is
+// hidden; it replaces 16 v_fmac_f64_dpp per step (bcast_acc).
+__device__ __forceinline__ void xi_mfma8(double (&X)[2], double zs, double vd) {
+    X[0] = __builtin_amdgcn_mfma_f64_4x4x4f64(zs, vd, X[0], 0, 0, 0);
+    X[1] = __builtin_amdgcn_mfma_f64_4x4x4f64(zs, dpp<0x141>(vd), X[1], 0, 0, 0);  // row_half_mirror
+}
+
 // S[i] += z(lane i) * w for every state i of the group
 template <int G, int N, int NS>
 __device__ __forceinline__ void bcast_acc(double (&S)[NS], double z, double w) {
@@ -355,6 +368,12 @@ __device__ void block_ll_partial(double lp, bool valid, double *sh, double *out)
 #define HMMBW_TAB_PAD 0
 #endif
 constexpr int kTabPad = HMMBW_TAB_PAD;
+#ifndef HMMBW_XI_MFMA
+#define HMMBW_XI_MFMA 1
+#endif
+#ifndef HMMBW_ZFULL
+#define HMMBW_ZFULL 1
+#endif
 constexpr int kHistOff = kTabPad ? 40960 : 32768;
 __host__ __device__ constexpr bool lds_tables_fit(int K, int GP) { return (size_t)K * GP * 16 <= (size_t)kHistOff; }
 __host__ __device__ constexpr size_t lds_table_bytes(int K, int GP) { return (size_t)kHistOff + (size_t)K * GP * 16; }
@@ -375,8 +394,15 @@ template <int N, int G, bool LR, bool LDSTAB, bool FWD_ONLY, bool DET = false>
 __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long bid, const long long nblk) {
     static_assert(!DET || (LDSTAB && !FWD_ONLY), "deterministic mode: E-step with LDS tables");
     constexpr int U = kWave / G;
-    constexpr int NS = LR ? 2 : N;      // per-lane S accumulators (row j of S)
-    constexpr int NV = NS + 3;          // + gamma_den_excl, gamma_den_all, pi_num
+    // dense G = 8: xi on the 4x4x4 MFMA (xi_mfma8), two accumulators per lane in its D layout
+    constexpr bool XM = !LR && G == 8 && !FWD_ONLY && HMMBW_XI_MFMA;
+    constexpr int NSR = LR ? 2 : N;     // S columns per state in the block reduction (row j of S)
+    constexpr int NS = XM ? 2 : NSR;    // per-lane S accumulators
+    constexpr int NV = NSR + 3;         // + gamma_den_excl, gamma_den_all, pi_num
+    // dense: the forward stores every z_t ([chunk][8 steps][64 lanes], kChunk x the checkpoint
+    // layout; the host sizes it), so the backward loads z instead of recomputing it: the recompute is
+    // 16 of the dense step's ~70 VALU instructions, the extra bytes stay mostly in L2/MALL
+    constexpr bool ZF = !LR && !FWD_ONLY && HMMBW_ZFULL;
     constexpr int GP = LDSTAB ? G + kTabPad : G;  // row stride of the emission / histogram tables
     // left-to-right with LDS tables: per (symbol, state) products {a_jj b_j(o), a_{j-1,j} b_j(o)}
     constexpr bool PT = LR && LDSTAB;
@@ -461,7 +487,7 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
         const int nch = (Tw + kChunk - 1) / kChunk;
         const long long symbase = a.L.wave_symoff[wave] + u * kChunk;  // pack index of this slot's chunk-0 entry
         const uint16_t *symw = a.L.sym + symbase;
-        double *ckw = a.ckpt + (FWD_ONLY ? 0 : a.L.wave_ckoff[wave]) + lane;
+        double *ckw = a.ckpt + (FWD_ONLY ? 0 : a.L.wave_ckoff[wave] * (ZF ? kChunk : 1)) + lane;
         uint4 *spw = a.spack + (FWD_ONLY ? 0 : a.L.wave_spoff[wave]) + u;
         const bool jv = j < N;
         // shortest sequence of the wave: in a ragged wave the chunks every lane is still inside of run
@@ -603,7 +629,8 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
                     }
                     sp[k] = st;
                     if constexpr (!FWD_ONLY)
-                        if (k == 0) ckw[(long long)c * kWave] = z;  // checkpoint z_{8c}
+                        if (ZF) ckw[((long long)c * kChunk + k) * kWave] = z;  // every z_t
+                        else if (k == 0) ckw[(long long)c * kWave] = z;    // checkpoint z_{8c}
                 }
                 if constexpr (!FWD_ONLY) spw[(long long)c * U] = pack_exps(sp);
             };
@@ -692,15 +719,32 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
                 // ring: chunk c - 4's are loaded as soon as chunk c is done with its slot; emissions
                 // through a 2-deep one; unrolled by 4 so no slot is copied (see the forward)
                 struct Ld {
-                    double ck;
+                    double ck;  // the checkpoint (not with ZF)
                     uint4 sp, pk;
                 };
                 auto ldset = [&](int c) -> Ld {
-                    return Ld{ckw[(long long)c * kWave], spw[(long long)c * U], loadpack(c)};
+                    Ld x;
+                    x.ck = ZF ? 0.0 : ckw[(long long)c * kWave];
+                    x.sp = spw[(long long)c * U];
+                    x.pk = loadpack(c);
+                    return x;
+                };
+                // ZF: the chunk's stored z_t through a 2-deep ring (chunk c - 2 loaded once chunk c is
+                // done; 4 deep would not fit 2 waves per SIMD)
+                double ZR[ZF ? 2 : 1][ZF ? kChunk : 1];
+                auto ldz = [&](double (&zz)[ZF ? kChunk : 1], int c) {
+                    if constexpr (ZF) {
+#pragma unroll
+                        for (int k = 0; k < kChunk; ++k) zz[k] = ckw[((long long)c * kChunk + k) * kWave];
+                    }
                 };
                 Ld X[4];
 #pragma unroll
                 for (int i = 0; i < 4; ++i) X[i] = ldset(cl - i >= 0 ? cl - i : 0);
+                if constexpr (ZF) {
+                    ldz(ZR[0], cl);
+                    ldz(ZR[ZF ? 1 : 0], cl >= 1 ? cl - 1 : 0);
+                }
                 Em E[2][kChunk];
                 double BU[2][kChunk];
                 // LDSTAB: this lane's table-row byte offsets of a chunk's symbols, computed once when the
@@ -724,7 +768,7 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
                 double f_hi = 0.0, fu_hi = 0.0;  // scaled emissions at o_{8c+8} (from chunk c+1)
                 Em e_hi{};                       // PT: product pair at o_{8c+8} ...
                 int s_hi = 0;                    // ... and that step's scale exponent
-                auto chunk = [&](int c, const Ld &cur, const uint4 &pkn, const Em (&bv)[kChunk],
+                auto chunk = [&](int c, const Ld &cur, const double (&zst)[ZF ? kChunk : 1], const uint4 &pkn, const Em (&bv)[kChunk],
                                  const double (&bu)[kChunk], Em (&bvn)[kChunk], double (&bun)[kChunk],
                                  const unsigned (&hac)[kChunk], unsigned (&han)[kChunk], auto MASK_) {
                     constexpr bool MASK = decltype(MASK_)::value;
@@ -744,10 +788,14 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
                     // the diagonal products ux[k] = a_jj b_j(o_{8c+k}) z_{8c+k-1}(j): xi_t(j,j) = ux[t+1] v_j
                     double zr[kChunk];
                     double ux[kChunk];
-                    zr[0] = cur.ck;
+                    zr[0] = ZF ? zst[0] : cur.ck;
                     ux[0] = 0.0;
 #pragma unroll
                     for (int k = 1; k < kChunk; ++k) {
+                        if constexpr (ZF) {
+                            zr[k] = zst[k];
+                            continue;
+                        }
                         double x;
                         if constexpr (PT) {
                             ux[k] = bv[k].x * zr[k - 1];
@@ -798,7 +846,8 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
                             double b0 = 0.0, b1 = 0.0;
                             if constexpr (G >= 4) {
                                 bcast_dot<G, N>(b0, b1, vd, arow);   // :182-193
-                                bcast_acc<G, N>(S, vd, zs);          // :402-408
+                                if constexpr (XM) xi_mfma8(S, zs, vd);  // :402-408
+                                else bcast_acc<G, N>(S, vd, zs);
                             } else {
                                 sfor<0, N>([&](auto I) {
                                     const double vk = gbcast<G, I.value>(vd, lane);
@@ -860,9 +909,10 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
                     constexpr int rn = (r + 1) & 3;
                     __builtin_amdgcn_sched_barrier(0);  // one chunk at a time: registers stay per chunk
                     CHUNKSTAMP(1, c);
-                    chunk(c, X[r], X[rn].pk, E[r & 1], BU[r & 1], E[(r + 1) & 1], BU[(r + 1) & 1], HA[r & 1],
-                          HA[(r + 1) & 1], MASK_);
+                    chunk(c, X[r], ZR[ZF ? (r & 1) : 0], X[rn].pk, E[r & 1], BU[r & 1], E[(r + 1) & 1], BU[(r + 1) & 1],
+                          HA[r & 1], HA[(r + 1) & 1], MASK_);
                     X[r] = ldset(c >= 4 ? c - 4 : 0);  // branch-free: exact vmcnt accounting
+                    if constexpr (ZF) ldz(ZR[r & 1], c >= 2 ? c - 2 : 0);
                 };
                 using Mk = std::integral_constant<bool, RAG>;  // only the first chunk is masked in full waves
                 using I0 = std::integral_constant<int, 0>;
@@ -926,7 +976,7 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
             PHASE(3);
             // xi_t(i,j) = a_ij * (the accumulated S_ij): scale once per sequence group (PT already
             // accumulates xi itself)
-            if constexpr (!PT) {
+            if constexpr (!PT && !XM) {  // XM: a_ij applied per element at the flush
 #pragma unroll
                 for (int k = 0; k < NS; ++k) {
                     if constexpr (LR) S[k] *= (k == 0 ? a_dg : a_up);
@@ -958,22 +1008,39 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
 
     if constexpr (!FWD_ONLY) if (!(a.ablate & 1)) {
         // ---- reduce per-lane accumulators over the U sequences of the wave, then the block ----
+        constexpr int K0 = XM ? NSR : 0;  // XM: the S columns come from the MFMA lanes below
         double vals[NV];
 #pragma unroll
-        for (int k = 0; k < NS; ++k) vals[k] = S[k];
-        vals[NS] = gex;
-        vals[NS + 1] = gall;
-        vals[NS + 2] = pin;
+        for (int k = 0; k < NS && !XM; ++k) vals[k] = S[k];
+        vals[NSR] = gex;
+        vals[NSR + 1] = gall;
+        vals[NSR + 2] = pin;
 #pragma unroll
-        for (int k = 0; k < NV; ++k) {
+        for (int k = K0; k < NV; ++k) {
             double x = vals[k];
             for (int m = G; m < kWave; m <<= 1) x += __shfl_xor(x, m);
             vals[k] = x;
         }
+        double xd = 0.0, xo = 0.0;
+        if constexpr (XM) {  // sum the two seq parities (lane bit 3)
+            xd = S[0] + __shfl_xor(S[0], 8);
+            xo = S[1] + __shfl_xor(S[1], 8);
+        }
         __syncthreads();
         if (u == 0) {
 #pragma unroll
-            for (int k = 0; k < NV; ++k) sRed[(wv * G + j) * NV + k] = vals[k];
+            for (int k = K0; k < NV; ++k) sRed[(wv * G + j) * NV + k] = vals[k];
+        }
+        if constexpr (XM) {
+            if ((lane & 8) == 0) {
+                const int jh = (lane >> 2) & 1, from = 4 * jh + (lane >> 4);
+                const int td = 4 * jh + (lane & 3), to = 4 * (1 - jh) + 3 - (lane & 3);
+                if (from < N) {
+                    const double *sA = sPA + G;  // xi_t(i,j) = a_ij S_ij
+                    if (td < N) sRed[(wv * G + from) * NV + td] = xd * sA[from * N + td];
+                    if (to < N) sRed[(wv * G + from) * NV + to] = xo * sA[from * N + to];
+                }
+            }
         }
         double *sPart = smem;  // DET: this workgroup's statistics [off_bnum] (the tables are dead now)
         if constexpr (DET)
@@ -989,13 +1056,13 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
             for (int w = 0; w < nw; ++w) x += sRed[(w * G + jj) * NV + k];
             if (x == 0.0) continue;
             long long dst;
-            if (k < NS) {
+            if (k < NSR) {
                 const int col = LR ? jj + k : k;
                 if (col >= N) continue;
                 dst = a.off_S + (long long)jj * N + col;
-            } else if (k == NS) {
+            } else if (k == NSR) {
                 dst = a.off_gex + jj;
-            } else if (k == NS + 1) {
+            } else if (k == NSR + 1) {
                 dst = a.off_gall + jj;
             } else {
                 dst = jj;  // pi_num at offset 0
@@ -1016,7 +1083,7 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
 }
 
 template <int N, int G, bool LR, bool LDSTAB, bool FWD_ONLY, bool DET = false>
-__global__ void __launch_bounds__(kBlock, LR ? 2 : 1) k_estep_small(EArgs a) {  // LR: 2 waves per SIMD (<= 256 VGPRs)
+__global__ void __launch_bounds__(kBlock, 2) k_estep_small(EArgs a) {  // 2 waves per SIMD (<= 256 VGPRs)
     estep_small_body<N, G, LR, LDSTAB, FWD_ONLY, DET>(a, blockIdx.x, gridDim.x);
 }
 
@@ -1025,7 +1092,7 @@ __global__ void __launch_bounds__(kBlock, LR ? 2 : 1) k_estep_small(EArgs a) {  
 // convergence state).  Replaces the per-word loop of HMM/main.py:147-152 (train) and the per-model
 // loop of HMM/hmm_testing.py:139-161 (test) with one launch per EM iteration / per scoring pass.
 template <int N, int G, bool LR, bool LDSTAB, bool FWD_ONLY>
-__global__ void __launch_bounds__(kBlock, LR ? 2 : 1) k_estep_small_group(GroupArgs g) {
+__global__ void __launch_bounds__(kBlock, 2) k_estep_small_group(GroupArgs g) {
     const long long b = blockIdx.x;
     int lo = 0, hi = g.nm - 1;  // the last model whose first workgroup is <= b (uniform search)
     while (lo < hi) {
