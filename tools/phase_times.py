@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--topology", default="left_to_right")
     ap.add_argument("--no-merge", action="store_true")
     ap.add_argument("--iters", type=int, default=6)
+    ap.add_argument("--kwaves", type=int, default=0, help="kernel waves to read (default: R / sequences per wave)")
     a = ap.parse_args()
     out_dir = os.path.join(ROOT, "gpurun_out", "phase")
     os.makedirs(out_dir, exist_ok=True)
@@ -59,6 +60,8 @@ def run_one(a, R, torch, BaumWelchEngine, default_initial_params, out_dir):
     torch.cuda.synchronize()
     U = 64 // (1 << max(1, (N - 1).bit_length()))
     nw = (R + U - 1) // U
+    if a.kwaves:
+        nw = a.kwaves
     nw_pad = ((nw + 3) // 4) * 4
     buf = np.zeros((nw_pad, 16), dtype=np.uint64)
     l = eng._lib
