@@ -99,7 +99,7 @@ def statistics_pass(eng, N, K, R):
     return g, ll, eng.params(normalise=False)
 
 
-def run_vs_oracle(oracle, R, T, N, K, topology, iters, seed, symbols="U"):
+def run_vs_oracle(oracle, R, T, N, K, topology, iters, seed, symbols="U", deterministic=False):
     from hmm_training_amd.engine import BaumWelchEngine, StatsLayout
     sym = _symbols(R, T, N, K, symbols, seed)
     off = np.arange(R + 1, dtype=np.int64) * T
@@ -107,7 +107,7 @@ def run_vs_oracle(oracle, R, T, N, K, topology, iters, seed, symbols="U"):
     pi, A, B = _params(N, K, topology, seed)
     ref = oracle.hmm_training(off, sym64, N, K, 0.0, iters, pi, A, B)
     assert ref.iterations == iters
-    with BaumWelchEngine(N, K, topology=topology) as eng:
+    with BaumWelchEngine(N, K, topology=topology, deterministic=deterministic) as eng:
         eng.set_observations(offsets=off, symbols=sym)
         eng.set_params(pi, A, B)
         assert eng.topology == topology
@@ -170,6 +170,18 @@ def test_cfg5_shard_full_size_vs_oracle(oracle_mt):
     run_vs_oracle(oracle_mt, 6_250, 400, 64, 1024, "dense", 2, seed=5)
 
 
+def test_cfg3_full_size_deterministic_vs_oracle(oracle_mt):
+    """cfg3 in deterministic-reduction mode (gamma rows + k_bnum_gather, per-workgroup partials +
+    k_det_reduce: no floating-point atomics), 3 EM iterations against the oracle."""
+    run_vs_oracle(oracle_mt, 10_000, 200, 8, 256, "left_to_right", 3, seed=31, deterministic=True)
+
+
+def test_cfg5_slice_deterministic_vs_oracle(oracle_mt):
+    """The wide path's deterministic mode (k_estep_mfma<.., DET>: every statistic in its owning lane,
+    per-tile partials) at cfg5's shape, 1,024 x 400, N=64, K=1024, 2 EM iterations against the oracle."""
+    run_vs_oracle(oracle_mt, 1024, 400, 64, 1024, "dense", 2, seed=56, deterministic=True)
+
+
 def test_cfg5_whole_on_one_gpu(oracle_mt):
     """BASELINE cfg5 unsharded: 50,000 x T=400, N=64, K=1024, dense on ONE GPU (20 GB of alpha_hat and
     gamma rows; the reference's per-utterance xi allocation, hmm_training.py:328-339, cannot run it), 2 EM
@@ -208,8 +220,9 @@ def test_cfg5_whole_on_one_gpu(oracle_mt):
     assert np.isclose(StatsLayout.lse_of_pairs(g["ll_pairs"]), oracle.lse(ll), rtol=1e-12)
 
 
-@pytest.mark.parametrize("xact", [None, "1", "3"])
-def test_spread_extra_waves_ragged_vs_oracle(oracle_mt, monkeypatch, xact):
+@pytest.mark.parametrize("xact,topology", [(None, "left_to_right"), ("1", "left_to_right"), ("3", "left_to_right"),
+                                           (None, "dense")])
+def test_spread_extra_waves_ragged_vs_oracle(oracle_mt, monkeypatch, xact, topology):
     """More waves than SIMDs (9,000 ragged sequences = 1,125 waves on 1,024 SIMDs): one full workgroup
     per CU, then workgroups of xact active waves (default 2; HMMBW_XACT forces 1 or 3), with inactive
     waves in them; every statistic and the trained model against the oracle (hmm_training.py:351-514)."""
@@ -220,9 +233,9 @@ def test_spread_extra_waves_ragged_vs_oracle(oracle_mt, monkeypatch, xact):
     R, N, K, iters = 9000, 8, 256, 3
     obs = [rng.integers(0, K, size=int(t)) for t in rng.integers(60, 160, size=R)]
     off, sym = to_csr(obs)
-    pi, A, B = _params(N, K, "left_to_right", 9)
+    pi, A, B = _params(N, K, topology, 9)
     ref = oracle_mt.hmm_training(off, sym.astype(np.int64), N, K, 0.0, iters, pi, A, B)
-    with BaumWelchEngine(N, K, topology="left_to_right") as eng:
+    with BaumWelchEngine(N, K, topology=topology) as eng:
         eng.set_observations(obs)
         eng.set_params(pi, A, B)
         eng.reset(0.0, iters)
