@@ -407,6 +407,16 @@ __global__ void __launch_bounds__(NT * 64, 2) k_estep_mfma(EArgs a) {  // 2 wave
     }
     __syncthreads();
     block_ll_partial(lp, ll_valid, sRed + NT * kTileSeqs, a.llpart + 2 * (long long)blockIdx.x);
+    if constexpr (!DET && !FWD_ONLY) {
+        // fused multi-rank launch (hmmbw_iterate / hmmbw_iterate_begin): the statistics went straight
+        // into the all-reduce buffer; the last tile to finish folds the tiles' (max, sum exp) pairs
+        // into this rank's slot (as the small kernels do), so no k_reduce_local pass is needed
+        if (a.rank_ll != nullptr) {
+            int ticket = 0;
+            if (threadIdx.x == 0) ticket = rank_ll_count(a);
+            if ((threadIdx.x >> 6) == 0 && __shfl(ticket, 0) == (int)(gridDim.x - 1)) rank_ll_fold(a, gridDim.x);
+        }
+    }
 }
 
 // B numerator of the wide kernels (:474-485): B_num[k][j] = sum of the gamma rows of every position

@@ -1066,7 +1066,7 @@ int hmmbw_mstep(hmmbw_ctx *c, double *stats_dev, int64_t n_seq_global) {
 // rank all-reduces the same buffer shape, also a rank whose shard is empty.
 static int mr_begin(hmmbw_ctx *c, long long n_seq_global, double **buf, long long *len) {
     if (c->ar_open) return fail(HMMBW_E_STATE, "an iteration is open (hmmbw_iterate_end first)");
-    const bool fused = !c->wide && !c->det;
+    const bool fused = !c->det;  // the small and the wide E-step accumulate into the all-reduce buffer
     if (fused) {
         // rounded to 256 B so all three buffers keep the copies' alignment (a 16-B shift splits the
         // B-numerator rows' 64-B segments over two cache lines; ~0.7 us per launch at cfg3)

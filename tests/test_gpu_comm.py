@@ -29,9 +29,9 @@ def rccl_path():
     ("dense", 5, 8, 256, 1e-6, None, False),
     ("left_to_right", 40, 5, 64, 1e-3, 1, False),      # converges before maxit (device-side stop rule)
     ("dense", 4, 8, 256, 1e-6, 3, False),
-    ("dense", 3, 40, 96, 1e-6, None, False),           # wide path: estep + k_reduce_local + all-reduce
+    ("dense", 3, 40, 96, 1e-6, None, False),           # wide path: E-step + gather into the all-reduce buffer
     ("left_to_right", 6, 8, 256, 1e-6, None, True),    # deterministic mode: partials, estep path
-    ("dense", 3, 40, 96, 1e-6, None, True),            # deterministic wide path
+    ("dense", 3, 40, 96, 1e-6, None, True),            # deterministic wide path: estep + k_reduce_local
 ])
 def test_native_comm_one_rank_matches_oracle(oracle, topology, maxit, N, K, eps, copies, det):
     from hmm_training_amd._lib import check, lib
@@ -58,7 +58,7 @@ def test_native_comm_one_rank_matches_oracle(oracle, topology, maxit, N, K, eps,
         ranks, ar_ms, ar_n = e.comm_info()
         assert ranks == 1 and ar_n >= st.iterations and ar_ms > 0  # chunks past convergence still all-reduce
         copy_len = N + N * N + 2 * N + K * N
-        if N <= 16 and not det:  # fused: the copies + one (max, sum exp) pair per rank, 256-B aligned
+        if not det:  # fused (small and wide): the copies + one (max, sum exp) pair per rank, 256-B aligned
             nc = copies or 2
             assert e.comm_payload_bytes() == 8 * (-(-(nc * copy_len + 2) // 32) * 32)
         else:

@@ -3,7 +3,7 @@ cuda:0.  hmmbw_iterate_begin / hmmbw_iterate_end split hmmbw_iterate at its nccl
 engine runs exactly the kernels an 8-GPU job runs (on the small kernels: the fused E-step that
 accumulates into the all-reduce buffer, the rank's (max, sum exp) pair at slot 2 * rank, the
 last-workgroup fold, the empty-shard memset, world-sized LL slots, the merged or standalone M-step on
-the all-reduced buffer; on the wide and deterministic paths: hmmbw_estep + k_reduce_local), and the
+the all-reduced buffer, small and wide; in deterministic mode: hmmbw_estep + k_reduce_local), and the
 test sums the W buffers in between (the all-reduce).
 
 Every rank must end on the reference's (pi, A, B) and L trace for the unsharded data
@@ -136,7 +136,7 @@ def test_split_iteration_empty_shards_present(hip):
 def test_split_iteration_multirank_vs_oracle(hip, oracle_mt, N, K, topology, R, tmax, world):
     """Every rank holds several workgroups (hundreds of sequences per rank): the per-rank last-workgroup fold over
     several workgroups, ranks' pairs at 2 * rank, world-sized LL slots; against the oracle run on the
-    unsharded data, 4 EM iterations (the wide N = 40 case takes hmmbw_estep + k_reduce_local)."""
+    unsharded data, 4 EM iterations (the wide N = 40 case: k_estep_mfma + k_bnum_gather into the buffer)."""
     from hmm_training_amd.engine import BaumWelchEngine, shard_bounds, to_csr
     from hmm_training_amd.hmm_training import default_initial_params
     oracle = oracle_mt
