@@ -401,7 +401,8 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
     constexpr int NV = NSR + 3;         // + gamma_den_excl, gamma_den_all, pi_num
     // dense: the forward stores every z_t ([chunk][8 steps][64 lanes], kChunk x the checkpoint
     // layout; the host sizes it), so the backward loads z instead of recomputing it: the recompute is
-    // 16 of the dense step's ~70 VALU instructions, the extra bytes stay mostly in L2/MALL
+    // 16 of the dense step's ~70 VALU instructions; the 128 MB at cfg3 go through HBM (275 MB of
+    // traffic per launch, 0.46 of the HBM peak over the kernel: not the bound, profiles/r3)
     constexpr bool ZF = !LR && !FWD_ONLY && HMMBW_ZFULL;
     constexpr int GP = LDSTAB ? G + kTabPad : G;  // row stride of the emission / histogram tables
     // left-to-right with LDS tables: per (symbol, state) products {a_jj b_j(o), a_{j-1,j} b_j(o)}
