@@ -65,7 +65,7 @@ template <int NT, bool FWD_ONLY, bool DET = false>
 __global__ void __launch_bounds__(NT * 64, 2) k_estep_mfma(EArgs a) {  // 2 waves per SIMD: <= 256 VGPRs
     static_assert(!(DET && FWD_ONLY), "deterministic mode is an E-step option");
     constexpr int NP = 16 * NT, KB = 4 * NT, IMG = NP * kXs;
-    extern __shared__ double smem[];
+    extern __shared__ __attribute__((aligned(256))) double smem[];  // 256-B aligned whatever the static LDS (ds_read_b128 rows)
     double *X0 = smem;                                   // [2][NP][kXs]: z (forward) / V (backward)
     // smem + 2 * IMG: [2][NP][kXs] masked z (backward xi operand), addressed as putb / topb + 2 * IMG
     double *sRed = smem + (FWD_ONLY ? 2 : 4) * IMG;      // [NT][16] partial sums + block LL scratch

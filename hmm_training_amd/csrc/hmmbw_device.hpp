@@ -407,7 +407,7 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
     constexpr int GP = LDSTAB ? G + kTabPad : G;  // row stride of the emission / histogram tables
     // left-to-right with LDS tables: per (symbol, state) products {a_jj b_j(o), a_{j-1,j} b_j(o)}
     constexpr bool PT = LR && LDSTAB;
-    extern __shared__ double smem[];
+    extern __shared__ __attribute__((aligned(256))) double smem[];  // 256-B aligned whatever the static LDS (ds_read_b128 rows)
     __shared__ double sPA[G + N * N];  // pi (zero-padded to G) and A of this iteration
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     PHASE(0);
