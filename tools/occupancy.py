@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--topology", default="left_to_right")
     ap.add_argument("--ablate", default="0")
     ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--copies", type=int, default=0, help="statistics copies (0: the engine default)")
     a = ap.parse_args()
     import torch
     from hmm_training_amd.engine import BaumWelchEngine
@@ -34,7 +35,8 @@ def main():
         B = rng.dirichlet(np.full(K, 2.0), size=N)
         if a.topology == "dense":
             A = 0.5 * A + 0.5 * rng.dirichlet(np.ones(N), size=N)
-        with BaumWelchEngine(N, K, topology=a.topology) as e:
+        kw = {"stat_copies": a.copies} if a.copies else {}
+        with BaumWelchEngine(N, K, topology=a.topology, **kw) as e:
             e.set_observations(offsets=np.arange(R + 1, dtype=np.int64) * T, symbols=sym)
             # steady state: back-to-back iterations with the merged M-step
             e.set_params(pi, A, B)

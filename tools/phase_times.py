@@ -73,11 +73,14 @@ def run_one(a, R, torch, BaumWelchEngine, default_initial_params, out_dir):
     us = lambda x: x / 100.0  # 100 MHz wall clock -> us
     names = ["start", "tables", "forward", "backward", "ll", "flush"]
     print(f"waves {nw}  kernel span {us(t[:, 5].max() - t0):.2f} us")
+    # waves that never stamp a phase in this launch (the idle waves of the spread map's xact-wave
+    # workgroups: their slots hold an earlier launch's stamps) are left out of that phase's statistics
     for k in range(1, 6):
-        d = us(t[:, k] - t[:, k - 1])
+        ok = (t[:, k] >= t0) & (t[:, k - 1] >= t0)
+        d = us(t[ok, k] - t[ok, k - 1])
         print(f"{names[k-1]:>8s}->{names[k]:<8s} mean {d.mean():7.2f}  p50 {np.median(d):7.2f}  max {d.max():7.2f} us")
     for k in range(6):
-        r = us(t[:, k] - t0)
+        r = us(t[t[:, k] >= t0, k] - t0)
         print(f"at {names[k]:<8s} rel-start  min {r.min():7.2f}  p50 {np.median(r):7.2f}  max {r.max():7.2f} us")
     if np.all(t[:, 6] > 0):  # merged M-step prologue: statistics gathered / tables built
         for k, nm in ((13, "zero-cleared"), (8, "mstep-entry"), (9, "stats-landed"), (6, "mstep-loads"),
