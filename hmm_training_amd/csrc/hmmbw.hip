@@ -33,6 +33,9 @@
 #include <dlfcn.h>
 
 #include <cstdlib>
+#include <map>
+#include <mutex>
+#include <tuple>
 #include <rccl/rccl.h>
 
 #include "hmmbw_device.hpp"
@@ -158,17 +161,91 @@ int fail(int code, const std::string &msg) {
             return fail(HMMBW_E_HIP, std::string(#expr) + ": " + hipGetErrorString(_e));         \
     } while (0)
 
+// Block cache of the small device buffers and the pinned snapshot blocks.  The drop-in API builds and
+// destroys one context per hmm_training call (HMM/hmm_training.py:265-267), and hipFree /
+// hipHostFree synchronise the device and return memory to the driver: a word-sized context (20
+// utterances) spent about 1 ms in hmmbw_ctx_destroy, as long as its 30 EM iterations.  Blocks up to
+// kCacheMaxBlock bytes are rounded up to a power of two and kept per (device, kind, size) for the next
+// context, up to kCacheMaxBytes per kind and device; larger buffers go straight to the driver.
+// Reused blocks are not cleared: every buffer is initialised by its owner, as after hipMalloc.
+constexpr size_t kCacheMaxBlock = size_t(4) << 20;
+constexpr size_t kCacheMaxBytes = size_t(256) << 20;
+struct BlockCache {
+    std::mutex mu;
+    std::map<std::tuple<int, int, size_t>, std::vector<void *>> free;  // (device, kind, bytes) -> blocks
+    std::map<void *, std::pair<int, size_t>> size_of;                   // cached-class block -> (kind, bytes)
+    std::map<std::pair<int, int>, size_t> held;                          // (device, kind) -> bytes cached
+};
+BlockCache &block_cache() {
+    static BlockCache *bc = new BlockCache;  // never destroyed: blocks may be released at process exit
+    return *bc;
+}
+size_t cache_class(size_t bytes) {
+    size_t c = 256;
+    while (c < bytes) c <<= 1;
+    return c;
+}
+enum { kDevBlock = 0, kPinnedBlock = 1 };
+hipError_t cached_alloc(void **p, size_t bytes, int kind) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (bytes > kCacheMaxBlock)
+        return kind == kDevBlock ? hipMalloc(p, bytes)
+                                 : hipHostMalloc(p, bytes, hipHostMallocMapped | hipHostMallocCoherent);
+    const size_t cls = cache_class(bytes);
+    BlockCache &bc = block_cache();
+    {
+        std::lock_guard<std::mutex> lk(bc.mu);
+        auto it = bc.free.find(std::make_tuple(dev, kind, cls));
+        if (it != bc.free.end() && !it->second.empty()) {
+            *p = it->second.back();
+            it->second.pop_back();
+            bc.held[std::make_pair(dev, kind)] -= cls;
+            return hipSuccess;
+        }
+    }
+    const hipError_t e = kind == kDevBlock ? hipMalloc(p, cls)
+                                           : hipHostMalloc(p, cls, hipHostMallocMapped | hipHostMallocCoherent);
+    if (e == hipSuccess) {
+        std::lock_guard<std::mutex> lk(bc.mu);
+        bc.size_of[*p] = std::make_pair(kind, cls);
+    }
+    return e;
+}
+void cached_free(void *p, int kind) {
+    if (!p) return;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    BlockCache &bc = block_cache();
+    {
+        std::lock_guard<std::mutex> lk(bc.mu);
+        auto it = bc.size_of.find(p);
+        if (it != bc.size_of.end()) {
+            const size_t cls = it->second.second;
+            size_t &held = bc.held[std::make_pair(dev, kind)];
+            if (held + cls <= kCacheMaxBytes) {
+                bc.free[std::make_tuple(dev, kind, cls)].push_back(p);
+                held += cls;
+                return;
+            }
+            bc.size_of.erase(it);
+        }
+    }
+    if (kind == kDevBlock) (void)hipFree(p);
+    else (void)hipHostFree(p);
+}
+
 template <class T>
 int dalloc(T **p, size_t n) {
     *p = nullptr;
     if (n == 0) n = 1;
-    HIP_TRY(hipMalloc(reinterpret_cast<void **>(p), n * sizeof(T)));
+    HIP_TRY(cached_alloc(reinterpret_cast<void **>(p), n * sizeof(T), kDevBlock));
     return HMMBW_OK;
 }
 
 template <class T>
 void dfree(T *&p) {
-    if (p) (void)hipFree(p);
+    cached_free(p, kDevBlock);
     p = nullptr;
 }
 
@@ -308,7 +385,15 @@ int set_device(hmmbw_ctx *c) {
     return HMMBW_OK;
 }
 
+// the block cache hands a freed block to the next allocation at once (hipFree used to synchronise the
+// device): the context's queued work must be done with a block before it is freed
+void sync_ctx(hmmbw_ctx *c) {
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    else (void)hipDeviceSynchronize();
+}
+
 void free_obs(hmmbw_ctx *c) {
+    sync_ctx(c);
     dfree(c->d_sym); dfree(c->d_wsym); dfree(c->d_wckoff); dfree(c->d_wspoff);
     dfree(c->d_wT); dfree(c->d_wfull); dfree(c->d_slen); dfree(c->d_sseq);
     dfree(c->d_ck); dfree(c->d_sp); dfree(c->d_ebuf); dfree(c->d_logp); dfree(c->d_llpart); dfree(c->d_zf);
@@ -317,6 +402,7 @@ void free_obs(hmmbw_ctx *c) {
 }
 
 int realloc_stats(hmmbw_ctx *c) {
+    sync_ctx(c);
     dfree(c->d_copies);
     c->pend.on = false;
     c->e_count = 0;
@@ -699,8 +785,8 @@ int hmmbw_ctx_destroy(hmmbw_ctx *c) {
     dfree(c->d_pi); dfree(c->d_A); dfree(c->d_B); dfree(c->d_Bt); dfree(c->d_out);
     for (auto &sn : c->snaps) {
         if (sn.ev) (void)hipEventDestroy(sn.ev);
-        if (sn.st) (void)hipHostFree(sn.st);
-        if (sn.hist) (void)hipHostFree(sn.hist);
+        cached_free(sn.st, kPinnedBlock);
+        cached_free(sn.hist, kPinnedBlock);
     }
     dfree(c->d_state); dfree(c->d_hist); dfree(c->d_copies); dfree(c->d_ext); dfree(c->d_xbuf); dfree(c->d_ctr);
     if (c->comm) {
@@ -1249,10 +1335,8 @@ int hmmbw_status_post(hmmbw_ctx *c, int64_t first, int64_t *ticket) {
     if (!sn.ev) {
         HIP_TRY(hipEventCreateWithFlags(&sn.ev, hipEventDisableTiming));
         // fine-grained host memory the snapshot kernel writes (visible once its event has completed)
-        const unsigned fl = hipHostMallocMapped | hipHostMallocCoherent;
-        HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&sn.st), sizeof(IterState), fl));
-        HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&sn.hist), sizeof(double) * 2 * (size_t)kHist,
-                              fl));
+        HIP_TRY(cached_alloc(reinterpret_cast<void **>(&sn.st), sizeof(IterState), kPinnedBlock));
+        HIP_TRY(cached_alloc(reinterpret_cast<void **>(&sn.hist), sizeof(double) * 2 * (size_t)kHist, kPinnedBlock));
     } else {
         HIP_TRY(hipEventSynchronize(sn.ev));  // the slot's previous snapshot has landed (two posts ago)
     }
@@ -1496,6 +1580,7 @@ int hmmbw_comm_init(hmmbw_ctx *c, const char *rccl_path, const void *id, int ran
     ncclComm_t comm = nullptr;
     ncclResult_t e = r->comm_init_rank(&comm, world, uid, rank);
     if (e != ncclSuccess) return rccl_fail(r, e, "ncclCommInitRank");
+    sync_ctx(c);
     dfree(c->d_ext);
     if (int rc = dalloc(&c->d_ext, (size_t)c->stats_len())) {
         (void)r->comm_destroy(comm);
