@@ -22,17 +22,20 @@ launcher, --gpus must equal WORLD_SIZE.  --dry-run runs the launcher/rendezvous/
 with no GPU work (CPU tests).
 
 Prints ONE JSON line (rank 0) with the driver's fields plus:
-  roofline     — achieved = algorithmic bytes per E-step launch (B_u = 24T + 16NT + 8
-                 per sequence) / the E-step kernel's mean duration from HIP events on its stream;
-                 traffic = measured HBM bytes per launch from the committed rocprofv3 PMC summary
-                 (profiles/), or null when none matches this config.  For N > 16 (the fp64-MFMA wide
-                 path, cfg5) the bound is "mfma": achieved = 8 N^2 T flops per sequence (the survey's
-                 figure) / kernel time against the 78.6 TFLOP/s dense fp64 matrix peak, with the
-                 fraction on the 6 N^2 T flops the kernel actually issues beside it.
+  roofline     — the BINDING ceiling of the E-step launch (roofline_bounds): of the bounds that apply,
+                 each written as achieved / peak of one resource, the one with the largest fraction:
+                 hbm (calibrated PMC bytes per launch from profiles/ over the kernel time, 8 TB/s),
+                 valu (all VALU instructions spread over the 1,024 SIMDs), simd_valu (the busiest SIMD's
+                 VALU pipe: ceil(waves / 1,024) waves' instructions, 4 cycles each at 2.4 GHz), and on
+                 the wide path (N > 16, cfg5) mfma / simd_mfma (the fp64 matrix pipe, 64 cycles per
+                 v_mfma_f64_16x16x4).  The kernel time is HIP events on the engine stream.  The SURVEY
+                 §8(d) byte model (B_u = 24T + 16NT + 8 per sequence) is kept as effective_bw_frac: it
+                 charges an alpha_hat round trip the kernels never make, so it can exceed 1.
   cpu_baseline — the oracle C restatement (oracle/bw_oracle.c, log domain like the reference) with
                  OpenMP over utterances on the host cores this process may use, timed on a bounded
                  sample of the same workload (rank 0, N=1 only), with its ratio to the reference's
-                 own NumPy path measured in the build container.
+                 own NumPy path measured in the build container, and the same-host ratio
+                 of the two (tests/golden/cpu_same_host.py -> profiles/*/cpu_same_host.json).
   comm         — N > 1: ranks of the RCCL communicator the engine created and the all-reduce
                  microseconds per iteration (HIP events around ncclAllReduce on the engine stream).
   synced       — SURVEY §8(d)'s protocol: median of per-iteration times with the 8-byte convergence
@@ -91,6 +94,9 @@ def parse(argv=None):
                    help="E-step launches timed one by one (HIP events) after the timed region")
     p.add_argument("--deterministic", action="store_true", help="fixed-order reductions (no fp atomics), bitwise reproducible")
     p.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) on MI355X; gloo only for tests")
+    p.add_argument("--allreduce", default="both", choices=["rccl", "peer", "both"],
+                   help="N > 1: the engine's all-reduce; both = time RCCL and the peer all-reduce side by side "
+                        "(same engine, same protocol) and report the faster as the headline")
     p.add_argument("--dry-run", action="store_true", help="launcher + rendezvous + timing skeleton, no GPU work")
     return p.parse_args(argv)
 
@@ -174,6 +180,8 @@ def find_traffic(cfg_key):
 SIMDS = 1024       # 256 CUs x 4 SIMDs (MI355X_MICROARCH.md chip-level parameters)
 VALU_CYCLES = 4    # wave64 fp64 VALU issue: 16 lanes per clock per SIMD (78.6 TF fp64 vector peak)
 CLOCK_MAX_GHZ = 2.4  # MI355X max shader clock: the issue bound at the peak clock is the optimistic one
+MFMA_F64_CYCLES = 64  # v_mfma_f64_16x16x4_f64: 2,048 flops per SIMD every 64 cycles (78.6 TF / 1,024 SIMDs / 2.4 GHz)
+MFMA_F64_FLOPS = 2 * 16 * 16 * 4
 
 
 def find_issue(cfg_key):
@@ -185,13 +193,75 @@ def find_issue(cfg_key):
                 d = json.load(fh)
         except Exception:
             continue
-        for k in d.values():
-            if isinstance(k, dict) and k.get("config_key") == cfg_key and k.get("SQ_INSTS_VALU"):
+        for name, k in d.items():
+            if isinstance(k, dict) and k.get("config_key") == cfg_key and k.get("SQ_INSTS_VALU") and "gather" not in name:
                 # GRBM_GUI_ACTIVE / 8 / kernel time reads high on dispatches under ~0.3 ms
                 # (MI355X_MICROARCH.md, DVFS give-back), so the bound is priced at the max clock
                 best = {"valu_insts_per_launch": float(k["SQ_INSTS_VALU"]), "clock_ghz": CLOCK_MAX_GHZ,
                         "clock_ghz_grbm_estimate": k.get("clock_ghz"), "source": os.path.relpath(path, ROOT)}
     return best
+
+
+def engine_waves(R, N):
+    """Active waves of one E-step launch and the pigeonhole minimum of the busiest SIMD's waves.
+    Small kernels (N <= 16): 64 / G sequences per wave, G = pow2ceil(N); wide (16 < N <= 64): tiles of
+    16 sequences with NP / 16 waves each (hmmbw.hip, hmmbw_set_observations)."""
+    if N <= 16:
+        G = 2 if N <= 2 else 4 if N <= 4 else 8 if N <= 8 else 16
+        waves = -(-R // (64 // G))
+    else:
+        waves = -(-R // 16) * (-(-N // 16))
+    return waves, -(-waves // SIMDS)
+
+
+def roofline_bounds(R, T, N, kern_s, traffic, issue, estep_s=None):
+    """Every ceiling that applies to the dominant launch, each as achieved / peak of ONE resource, so every
+    frac is <= 1 when the measurement and the model are right; the binding bound is the largest frac.
+
+    hbm        measured HBM bytes per launch (calibrated PMC FETCH/WRITE, profiles/) / kernel time vs 8 TB/s.
+    valu       all VALU instructions of the launch (SQ_INSTS_VALU) spread evenly over the 1,024 SIMDs,
+               4 cycles each (wave64 over 16 lanes) at the 2.4 GHz max clock.
+    simd_valu  the busiest SIMD's VALU pipe: by pigeonhole some SIMD runs ceil(waves / 1,024) waves, and it
+               must issue all their VALU instructions one after another (a SIMD's single VALU pipe), so
+               achieved = its issue rate over the kernel, peak = clock / 4.
+    mfma, simd_mfma  (wide path) the same for the fp64 matrix pipe: every wave issues 48 dependent-block
+               v_mfma_f64_16x16x4 per step (forward 4NT, backward 4NT, xi 4NT at NT = 4), 64 cycles each.
+    """
+    waves, wmax = engine_waves(R, N)
+    t_clock = CLOCK_MAX_GHZ * 1e9
+    out = {"waves_per_launch": waves, "waves_on_busiest_simd": wmax, "clock_ghz": CLOCK_MAX_GHZ}
+    if traffic and kern_s > 0:
+        ach = traffic[0] / kern_s / 1e9
+        out["hbm"] = {"achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
+                      "bytes_per_launch": traffic[0], "source": traffic[1]}
+    if N > 16:
+        nt = -(-N // 16)
+        mfma_wave = 3 * 4 * nt * T  # per step: forward 4NT, backward 4NT, xi NT x 4 (estep_mfma.hpp)
+        t_e = estep_s if estep_s else kern_s
+        peak_simd = t_clock / MFMA_F64_CYCLES * MFMA_F64_FLOPS / 1e12  # TFLOP/s of one SIMD's matrix pipe
+        ach_bal = waves * mfma_wave * MFMA_F64_FLOPS / t_e / 1e12
+        out["mfma"] = {"achieved": ach_bal, "peak": peak_simd * SIMDS, "unit": "TFLOP/s",
+                       "frac": ach_bal / (peak_simd * SIMDS), "mfma_per_wave": mfma_wave,
+                       "kernel": "k_estep_mfma", "kernel_ms": 1e3 * t_e}
+        ach_s = wmax * mfma_wave * MFMA_F64_FLOPS / t_e / 1e12
+        out["simd_mfma"] = {"achieved": ach_s, "peak": peak_simd, "unit": "TFLOP/s per SIMD",
+                            "frac": ach_s / peak_simd, "mfma_per_wave": mfma_wave,
+                            "t_bound_us": 1e6 * wmax * mfma_wave * MFMA_F64_CYCLES / t_clock,
+                            "kernel": "k_estep_mfma", "kernel_ms": 1e3 * t_e}
+    if issue and kern_s > 0 and N <= 16:
+        per_wave = issue["valu_insts_per_launch"] / waves
+        peak = t_clock / VALU_CYCLES / 1e9  # G VALU instructions / s of one SIMD
+        ach_bal = issue["valu_insts_per_launch"] / SIMDS / kern_s / 1e9
+        out["valu"] = {"achieved": ach_bal, "peak": peak, "unit": "G VALU instr/s per SIMD (mean)",
+                       "frac": ach_bal / peak, "valu_per_launch": issue["valu_insts_per_launch"],
+                       "source": issue["source"]}
+        ach_s = wmax * per_wave / kern_s / 1e9
+        out["simd_valu"] = {"achieved": ach_s, "peak": peak, "unit": "G VALU instr/s (busiest SIMD)",
+                            "frac": ach_s / peak, "valu_per_wave": per_wave,
+                            "t_bound_us": 1e6 * wmax * per_wave * VALU_CYCLES / t_clock, "source": issue["source"]}
+    cands = {k: v for k, v in out.items() if isinstance(v, dict) and "frac" in v}
+    out["binding"] = max(cands, key=lambda k: cands[k]["frac"]) if cands else None
+    return out
 
 
 def host_threads(requested=0):
@@ -243,14 +313,43 @@ def cpu_baseline(N, K, T, topology, budget_s, seed, symbols="U", threads=0):
     finally:
         O.set_threads(1)
     value = R / dt
-    return {"value": value, "unit": "utterances/s/iter", "cores": nth, "kind": "port",
-            "cpu_model": cpu_model(), "nproc_visible": os.cpu_count(),
-            "sample": f"{R} sequences x 1 EM iteration (T={T}, N={N}, K={K}, {topology}, symbols {symbols}) on the "
-                      f"oracle restatement oracle/bw_oracle.c, OpenMP over utterances on {nth} threads, {dt:.1f} s",
-            "ratio_vs_reference_8cores": value / REF_UTT_PER_S_8CORES,
-            "ratio_per_core_vs_reference": (value / nth) / REF_UTT_PER_S_1CORE,
-            "reference_note": "reference NumPy path (HMM/hmm_training.py) measured in the build container at cfg3 "
-                              "shape: 9.39 utt/s/iter on 1 core, 79.98 on 8 (BASELINE.md); different host"}
+    out = {"value": value, "unit": "utterances/s/iter", "cores": nth, "kind": "port",
+           "cpu_model": cpu_model(), "nproc_visible": os.cpu_count(),
+           "sample": f"{R} sequences x 1 EM iteration (T={T}, N={N}, K={K}, {topology}, symbols {symbols}) on the "
+                     f"oracle restatement oracle/bw_oracle.c, OpenMP over utterances on {nth} threads, {dt:.1f} s",
+           "ratio_vs_reference_8cores": value / REF_UTT_PER_S_8CORES,
+           "ratio_per_core_vs_reference": (value / nth) / REF_UTT_PER_S_1CORE,
+           "reference_note": "reference NumPy path (HMM/hmm_training.py) measured in the build container at cfg3 "
+                             "shape: 9.39 utt/s/iter on 1 core, 79.98 on 8 (BASELINE.md); different host"}
+    same = find_same_host()
+    if same and (T, N, K) == (200, 8, 256):
+        # the reference and the oracle timed back to back on ONE host (tests/golden/cpu_same_host.py): the
+        # oracle's per-core speed-up over the reference there, and what it implies for the reference on
+        # this box's cores (the reference itself cannot run here)
+        r = same["ratio_oracle_vs_reference_per_core"]
+        out["same_host"] = {"host": same["host"], "source": same["source"],
+                            "reference_utt_per_s_1core": same["reference_utt_per_s_1core"],
+                            "oracle_utt_per_s_1thread": same["oracle_utt_per_s_1thread"],
+                            "ratio_oracle_vs_reference_per_core": r,
+                            "reference_estimate_here_utt_per_s": value / r,
+                            "note": "reference_estimate_here = this box's oracle rate on "
+                                    f"{nth} threads / the same-host per-core ratio (assumes the reference, "
+                                    "single-threaded NumPy, would scale over processes as the oracle over threads)"}
+    return out
+
+
+def find_same_host():
+    """The latest committed same-host timing of the reference vs the oracle (profiles/*/cpu_same_host.json)."""
+    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "cpu_same_host.json")))
+    if not paths:
+        return None
+    try:
+        with open(paths[-1]) as fh:
+            d = json.load(fh)
+    except Exception:
+        return None
+    d["source"] = os.path.relpath(paths[-1], ROOT)
+    return d
 
 
 def free_port():
@@ -324,7 +423,7 @@ def main(argv=None):
     pi, A, B = init_params(N, K, topo, np.random.default_rng(seed))
 
     eng = BaumWelchEngine(N, K, device=device, topology=topo, rank=rank, world_size=world,
-                          deterministic=args.deterministic)
+                          deterministic=args.deterministic, allreduce=args.allreduce)
     t_up = time.perf_counter()
     eng.set_observations(offsets=offsets, symbols=symbols, n_seq_global=R * world)
     eng.set_params(pi, A, B)
@@ -333,47 +432,76 @@ def main(argv=None):
     assert eng.topology == topo
     eng.reset(0.0, 1 << 40)  # epsilon 0: no early stop, every timed step is a full iteration
     stats = eng.make_stats_buffer() if world > 1 and not eng.native_comm else None
+    n_iter = [0]
 
-    eng.enqueue_iterations(args.warmup, stats)
-    torch.cuda.synchronize()
-    eng.timing(0)
-    eng.comm_info(reset=True)
-    # The engine launches on torch's current stream (BaumWelchEngine binds it), so one event pair on
-    # that stream around the whole timed region gives the GPU time per step without perturbing it.
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    ev0.record()
-    for _ in range(args.steps):
-        eng.enqueue_iterations(1, stats)
-    ev1.record()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    gpu_ms_step = ev0.elapsed_time(ev1) / args.steps
-    st, _ = eng.status()
-    if st.iterations != args.warmup + args.steps:
-        raise RuntimeError(f"expected {args.warmup + args.steps} iterations, engine ran {st.iterations}")
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{device}")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    # E-step launches timed one by one (event pairs around each launch serialise the queue, so this
-    # reads ~1-2 us above the undisturbed kernel), in a separate batch after the timed region; plus the
-    # all-reduce per iteration on the engine communicator
-    kern_ms = ar_ms = 0.0
-    kern_n = ar_n = 0
-    comm_ranks = eng.comm_info()[0]
-    if not args.no_kernel_timing:
-        eng.timing(1)
-        eng.comm_info(reset=True)
-        eng.enqueue_iterations(args.timing_batch, stats)
+    def enqueue(n):
+        eng.enqueue_iterations(n, stats)
+        n_iter[0] += n
+
+    def leg(steps, warmup):
+        """Warm-up, then EXACTLY `steps` EM iterations between barrier + synchronize brackets (max over
+        ranks), then the per-launch timing batch (HIP events) outside the timed region."""
+        enqueue(warmup)
         torch.cuda.synchronize()
-        kern_ms, kern_n = eng.timing(0)
-        comm_ranks, ar_ms, ar_n = eng.comm_info(reset=True)
+        eng.timing(0)
+        eng.comm_info(reset=True)
+        # The engine launches on torch's current stream (BaumWelchEngine binds it), so one event pair on
+        # that stream around the whole timed region gives the GPU time per step without perturbing it.
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ev0.record()
+        for _ in range(steps):
+            enqueue(1)
+        ev1.record()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+        r = {"gpu_ms_step": ev0.elapsed_time(ev1) / steps, "kern_ms": 0.0, "kern_n": 0, "est_ms": 0.0, "est_n": 0,
+             "ar_ms": 0.0, "ar_n": 0}
+        st, _ = eng.status()
+        if st.iterations != n_iter[0]:
+            raise RuntimeError(f"expected {n_iter[0]} iterations, engine ran {st.iterations}")
+        if world > 1:
+            t = torch.tensor([elapsed], dtype=torch.float64,
+                             device=f"cuda:{device}" if args.dist_backend == "nccl" else "cpu")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elapsed = float(t.item())
+        r["elapsed"] = elapsed
+        r["comm_ranks"] = eng.comm_info()[0]
+        # E-step launches timed one by one (event pairs around each launch serialise the queue, so this
+        # reads ~1-2 us above the undisturbed kernel), in a separate batch after the timed region; plus the
+        # all-reduce per iteration on the engine's own path
+        if not args.no_kernel_timing:
+            eng.timing(1)
+            eng.comm_info(reset=True)
+            enqueue(args.timing_batch)
+            torch.cuda.synchronize()
+            r["est_ms"], r["est_n"] = eng.timing_split()  # wide path: the E-step kernel alone (before the gather)
+            r["kern_ms"], r["kern_n"] = eng.timing(0)
+            r["comm_ranks"], r["ar_ms"], r["ar_n"] = eng.comm_info(reset=True)
+        r["allreduce"] = eng.allreduce
+        return r
+
+    legs = {}
+    first = leg(args.steps, args.warmup)
+    legs[first["allreduce"] or "none"] = first
+    if world > 1 and args.allreduce == "both" and eng._rccl_ok and eng._peer_ok:
+        # the other all-reduce on the same engine and data, same protocol: both are measured side by side
+        other = "peer" if first["allreduce"] == "rccl" else "rccl"
+        eng.set_allreduce(other)
+        legs[other] = leg(args.steps, max(2, min(args.warmup, 10)))
+    # the headline is the faster leg (both run the full EM iteration; config.allreduce names it)
+    best = max(legs, key=lambda k: -legs[k]["elapsed"])
+    L = legs[best]
+    eng.set_allreduce(best) if best in ("rccl", "peer") and len(legs) > 1 else None
+    elapsed, gpu_ms_step = L["elapsed"], L["gpu_ms_step"]
+    kern_ms, kern_n, est_ms, est_n = L["kern_ms"], L["kern_n"], L["est_ms"], L["est_n"]
+    ar_ms, ar_n, comm_ranks = L["ar_ms"], L["ar_n"], L["comm_ranks"]
+    st, _ = eng.status()
 
     synced = None
     if not args.no_synced:
@@ -394,37 +522,36 @@ def main(argv=None):
     wide = N > 16
     cfg_key = f"R{R}_T{T}_N{N}_K{K}_{topo}" + ("_H" if args.symbols == "H" else "")
     traffic = find_traffic(cfg_key)
-    if wide:  # fp64 MFMA recursions (estep_mfma.hpp): priced against the dense fp64 matrix peak
-        achieved = flops_per_sequence(T, N) * R / kern_s / 1e12 if kern_s > 0 else float("nan")
-        issued = mfma_flops_issued(T, N) * R / kern_s / 1e12 if kern_s > 0 else float("nan")
-        roof = {"bound": "mfma", "achieved": achieved, "peak": FP64_MFMA_PEAK_TFS, "unit": "TFLOP/s",
-                "frac": achieved / FP64_MFMA_PEAK_TFS, "traffic": traffic[0] if traffic else None,
-                "kernel": "k_estep_mfma + k_bnum_gather (E-step)", "kernel_ms": kern_s * 1000.0,
-                "kernel_time_source": kern_src,
-                "flops_per_launch_algorithmic": flops_per_sequence(T, N) * R,
-                "issued_tflops_6N2T": issued, "frac_issued_6N2T": issued / FP64_MFMA_PEAK_TFS,
-                "traffic_source": traffic[1] if traffic else None}
-    else:
-        achieved = bu * R / kern_s / 1e9 if kern_s > 0 else float("nan")
-        roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS, "traffic": traffic[0] if traffic else None,
-                "kernel": "k_estep_small (E-step)", "kernel_ms": kern_s * 1000.0,
-                "kernel_time_source": kern_src,
-                "bytes_per_launch_algorithmic": bu * R,
-                "traffic_source": traffic[1] if traffic else None}
-    # measured-HBM fraction: the PMC bytes per launch (profiles/) over the kernel time -- what the
-    # memory system actually carries (the byte model counts every alpha/beta element once; the
-    # kernel keeps checkpoints, packs and tables on chip)
-    roof["hbm_frac_measured"] = (traffic[0] / kern_s / (HBM_PEAK_GBS * 1e9)) if (traffic and kern_s > 0) else None
     issue = find_issue(cfg_key)
-    if issue and kern_s > 0 and not wide:  # VALU-issue bound from the committed SQ counters (profiles/)
-        t_issue = issue["valu_insts_per_launch"] * VALU_CYCLES / (SIMDS * issue["clock_ghz"] * 1e9)
-        roof["valu_issue_bound"] = {"t_us": 1e6 * t_issue, "frac": t_issue / kern_s, **issue,
-                                    "model": f"SQ_INSTS_VALU per launch x {VALU_CYCLES} cycles (wave64 fp64 issue) / "
-                                             f"({SIMDS} SIMDs x clock): the time if every SIMD issued VALU "
-                                             "back to back with the work perfectly balanced"}
-    roof["gpu_ms_per_step"] = gpu_ms_step
-    roof["kernel_ms_per_launch_events"] = kern_ms / kern_n if kern_n else None
+    estep_s = (est_ms / est_n / 1000.0) if est_n else None
+    bounds = roofline_bounds(R, T, N, kern_s, traffic, issue, estep_s)
+    # The roofline is the binding ceiling among the bounds that apply (largest achieved / peak).  The
+    # SURVEY §8(d) byte model (B_u = 24T + 16NT + 8 per sequence over the launch) is kept beside it as
+    # effective_bw_frac: it charges an alpha_hat HBM round trip the checkpoint-and-recompute kernels never
+    # make, so on the small kernels it exceeds 1 and bounds nothing.
+    b = bounds.get(bounds.get("binding") or "", None)
+    if wide:
+        eff = flops_per_sequence(T, N) * R / kern_s / 1e12 if kern_s > 0 else float("nan")
+        eff_model = {"effective_tflops_8N2T": eff, "effective_frac_8N2T": eff / FP64_MFMA_PEAK_TFS,
+                     "issued_frac_6N2T": mfma_flops_issued(T, N) * R / kern_s / 1e12 / FP64_MFMA_PEAK_TFS,
+                     "flops_per_launch_algorithmic": flops_per_sequence(T, N) * R}
+        eff_frac = eff / FP64_MFMA_PEAK_TFS
+    else:
+        eff = bu * R / kern_s / 1e9 if kern_s > 0 else float("nan")
+        eff_model = {"effective_bw_gbs": eff, "bytes_per_launch_algorithmic": bu * R,
+                     "model": "SURVEY §8(d): 24T + 16NT + 8 bytes per sequence"}
+        eff_frac = eff / HBM_PEAK_GBS
+    roof = {"bound": bounds.get("binding") or ("mfma" if wide else "hbm"),
+            "achieved": b["achieved"] if b else None, "peak": b["peak"] if b else None,
+            "unit": b["unit"] if b else None, "frac": b["frac"] if b else None,
+            "traffic": traffic[0] if traffic else None,
+            "kernel": "k_estep_mfma + k_bnum_gather (E-step)" if wide else "k_estep_small (E-step)",
+            "kernel_ms": kern_s * 1000.0, "kernel_time_source": kern_src,
+            "effective_bw_frac": eff_frac, "byte_model": eff_model,
+            "hbm_frac_measured": bounds["hbm"]["frac"] if "hbm" in bounds else None,
+            "bounds": bounds, "traffic_source": traffic[1] if traffic else None,
+            "gpu_ms_per_step": gpu_ms_step,
+            "kernel_ms_per_launch_events": kern_ms / kern_n if kern_n else None}
 
     if rank == 0:
         out = {
@@ -446,12 +573,19 @@ def main(argv=None):
                        "sequences_per_gpu": R, "sequences_total": R * world, "T": T, "N": N, "K": K,
                        "topology": topo, "symbols": args.symbols, "deterministic": bool(args.deterministic),
                        "parallelism": f"dp{world}" if world > 1 else "single",
-                       "allreduce": ("rccl (engine communicator, engine stream)" if eng.native_comm else
-                                     f"torch.distributed ({args.dist_backend})") if world > 1 else None},
+                       "allreduce": ({"rccl": "rccl (engine communicator, engine stream)",
+                                      "peer": "peer (engine push / wait + sum over IPC-mapped regions, engine stream)"}
+                                     .get(best, f"torch.distributed ({args.dist_backend})")) if world > 1 else None},
             "roofline": roof,
-            "comm": {"rccl_comm_ranks": comm_ranks, "allreduce_us_per_iter": 1000.0 * ar_ms / ar_n if ar_n else None,
+            "comm": {"kind": best, "rccl_comm_ranks": comm_ranks,
+                     "allreduce_us_per_iter": 1000.0 * ar_ms / ar_n if ar_n else None,
                      "allreduce_timed": ar_n,
-                     "payload_bytes": eng.comm_payload_bytes() if eng.native_comm else 8 * eng.stats_len}
+                     "payload_bytes": eng.comm_payload_bytes() if eng.native_comm else 8 * eng.stats_len,
+                     "legs": {k: {"value": R * world * args.steps / v["elapsed"],
+                                  "ms_per_step": 1000.0 * v["elapsed"] / args.steps,
+                                  "allreduce_us_per_iter": 1000.0 * v["ar_ms"] / v["ar_n"] if v["ar_n"] else None,
+                                  "kernel_ms_per_launch_events": v["kern_ms"] / v["kern_n"] if v["kern_n"] else None}
+                              for k, v in legs.items()}}
             if world > 1 else None,
             "synced": synced,
             "upload_s": upload_s,
@@ -490,7 +624,8 @@ def synced_protocol(eng, stats, world, dist, R, iters=10, dropin_iters=20):
     dt = time.perf_counter() - t0
     med = float(np.median(per))
     if world > 1:
-        t = torch.tensor([med, dt], dtype=torch.float64, device=f"cuda:{eng.device}")
+        t = torch.tensor([med, dt], dtype=torch.float64,
+                         device=f"cuda:{eng.device}" if dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         med, dt = float(t[0]), float(t[1])
     return {"median_ms_per_iter_with_d2h": 1000.0 * med, "utt_per_s_with_d2h": R * world / med,

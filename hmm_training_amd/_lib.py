@@ -23,6 +23,7 @@ HMMBW_E_UNSUPPORTED = -3
 HMMBW_E_STATE = -4
 HMMBW_E_EMPTY_SEQUENCE = -5
 HMMBW_E_SYMBOL_RANGE = -6
+HMMBW_E_TIMEOUT = -7
 
 TOPOLOGY = {"auto": 0, "dense": 1, "left_to_right": 2}
 TOPOLOGY_NAME = {v: k for k, v in TOPOLOGY.items()}
@@ -37,13 +38,18 @@ EXPORTED = (
     "hmmbw_set_option", "hmmbw_group_create", "hmmbw_group_destroy", "hmmbw_group_iterate", "hmmbw_group_score",
     "hmmbw_group_timing", "hmmbw_vq_encode", "hmmbw_comm_unique_id", "hmmbw_comm_init",
     "hmmbw_comm_probe", "hmmbw_comm_info", "hmmbw_comm_payload", "hmmbw_iterate_begin", "hmmbw_iterate_end",
+    "hmmbw_cache_trim", "hmmbw_timing_split", "hmmbw_peer_region", "hmmbw_peer_ipc_handle", "hmmbw_peer_open",
+    "hmmbw_peer_attach", "hmmbw_allreduce_kind",
 )
-ABI_VERSION = 2
+ABI_VERSION = 3
 OPT_SAFE_SCALING = 1
 OPT_ABLATE = 2
 OPT_STAT_COPIES = 3
 OPT_MERGE_MSTEP = 4
 OPT_DETERMINISTIC = 7
+OPT_ALLREDUCE = 8
+OPT_PEER_TIMEOUT_MS = 9
+ALLREDUCE = {"rccl": 0, "peer": 1}
 
 
 class HMMBWError(RuntimeError):
@@ -72,6 +78,7 @@ def _declare(lib):
         "hmmbw_abi_version": (ctypes.c_int, []),
         "hmmbw_last_error": (ctypes.c_char_p, []),
         "hmmbw_device_count": (ctypes.c_int, [P(ctypes.c_int)]),
+        "hmmbw_cache_trim": (ctypes.c_int, [P(ctypes.c_int64)]),
         "hmmbw_ctx_create": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, P(c_ctx)]),
         "hmmbw_ctx_destroy": (ctypes.c_int, [c_ctx]),
         "hmmbw_set_stream": (ctypes.c_int, [c_ctx, ctypes.c_void_p]),
@@ -95,6 +102,12 @@ def _declare(lib):
         "hmmbw_get_loglik": (ctypes.c_int, [c_ctx, ctypes.c_void_p]),
         "hmmbw_score": (ctypes.c_int, [c_ctx, ctypes.c_void_p]),
         "hmmbw_timing": (ctypes.c_int, [c_ctx, ctypes.c_int, P(ctypes.c_double), P(ctypes.c_int64)]),
+        "hmmbw_timing_split": (ctypes.c_int, [c_ctx, P(ctypes.c_double), P(ctypes.c_int64)]),
+        "hmmbw_peer_region": (ctypes.c_int, [c_ctx, P(ctypes.c_void_p), P(ctypes.c_int64)]),
+        "hmmbw_peer_ipc_handle": (ctypes.c_int, [c_ctx, ctypes.c_void_p]),
+        "hmmbw_peer_open": (ctypes.c_int, [c_ctx, ctypes.c_void_p, ctypes.c_int64]),
+        "hmmbw_peer_attach": (ctypes.c_int, [c_ctx, ctypes.c_void_p, ctypes.c_int64]),
+        "hmmbw_allreduce_kind": (ctypes.c_int, [c_ctx, P(ctypes.c_int)]),
         "hmmbw_set_option": (ctypes.c_int, [c_ctx, ctypes.c_int, ctypes.c_int64]),
         "hmmbw_vq_encode": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int,
                                            ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
@@ -135,6 +148,13 @@ def lib():
                                   "`python -m hmm_training_amd.build`)")
             _lib = handle
     return _lib
+
+
+def cache_trim() -> int:
+    """Return the library's cached device / pinned blocks to the driver (hmmbw_cache_trim); bytes freed."""
+    n = ctypes.c_int64()
+    check(lib().hmmbw_cache_trim(ctypes.byref(n)))
+    return n.value
 
 
 def check(rc: int) -> None:

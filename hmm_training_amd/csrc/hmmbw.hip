@@ -133,6 +133,91 @@ __global__ void k_finalise(const double *pi, const double *A, const double *B, i
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Peer all-reduce (HMMBW_OPT_ALLREDUCE = 1; include/hmmbw.h).  The reference's sums over all recordings
+// (hmm_training.py:415-424 pi over the global R, :429-500 A and B, :503 L) become ONE elementwise sum of
+// the ranks' statistics buffers per EM iteration.  Every rank owns a receive region in its HBM:
+//   [2 iteration parities][world slots][slot doubles], then flags [world][chunks] (uint64 sequence numbers)
+// k_peer_push  (after the E-step): workgroup (chunk c, peer p) writes chunk c of this rank's buffer into
+//              slot `rank` of p's region with system-scope write-through stores, waits for them
+//              (vmcnt(0) in every wave, then the barrier) and release-stores the iteration's sequence
+//              number into p's flag (rank, c);
+// k_peer_reduce (before the M-step): workgroup c's first wave polls its region's W flags of chunk c
+//              (system-scope loads + s_sleep, bounded by wall-clock ticks: on expiry the iteration
+//              state records HMMBW_E_TIMEOUT and stops EM), then sums the W slots in rank order into
+//              the buffer, so every rank holds bitwise-identical sums.
+// Parity double-buffering is enough: a rank can push iteration e + 2 into p's slot only after its own
+// reduce of e + 1, which needs p's push of e + 1, which p enqueues after its reduce of e.
+// ---------------------------------------------------------------------------------------------
+constexpr int kMaxPeers = 16;
+constexpr int kPeerChunk = 256;  // doubles per chunk = threads per workgroup
+
+struct PeerArgs {
+    double *region[kMaxPeers];  // every rank's receive region, as addressable from this device
+    long long n;                // payload doubles
+    long long slot;             // slot stride (n rounded up to 256 B)
+    long long nch;              // chunks of kPeerChunk doubles
+    int world, rank;
+};
+
+__device__ __forceinline__ unsigned long long *peer_flags(double *region, const PeerArgs &P) {
+    return reinterpret_cast<unsigned long long *>(region + 2LL * P.world * P.slot);
+}
+
+__global__ void __launch_bounds__(kPeerChunk) k_peer_push(const double *src, PeerArgs P, unsigned long long seq,
+                                                          const IterState *state) {
+    if (state->done) return;  // identical on every rank: no rank pushes, none waits
+    const long long c = blockIdx.x;
+    const int p = blockIdx.y;
+    const long long i = c * kPeerChunk + threadIdx.x;
+    double *dst = P.region[p] + ((long long)(seq & 1) * P.world + P.rank) * P.slot;
+    if (i < P.n) __hip_atomic_store(dst + i, src[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's write-through stores are acknowledged
+    __syncthreads();
+    if (threadIdx.x == 0)
+        __hip_atomic_store(peer_flags(P.region[p], P) + (long long)P.rank * P.nch + c, seq, __ATOMIC_RELEASE,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ void __launch_bounds__(kPeerChunk) k_peer_reduce(double *dst, PeerArgs P, unsigned long long seq,
+                                                            IterState *state, long long timeout_ticks) {
+    __shared__ int ok;
+    if (state->done) return;
+    const long long c = blockIdx.x;
+    const int tid = threadIdx.x;
+    double *reg = P.region[P.rank];
+    if (tid < 64) {  // one wave polls: lane q watches rank q's flag of this chunk
+        const unsigned long long *fl = peer_flags(reg, P) + c;
+        bool got = tid >= P.world;
+        const unsigned long long t0 = wall_clock64();
+        while (true) {
+            if (!got) got = __hip_atomic_load(fl + (long long)tid * P.nch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >= seq;
+            if (__all(got)) break;
+            if ((long long)(wall_clock64() - t0) > timeout_ticks) break;
+            __builtin_amdgcn_s_sleep(2);
+        }
+        const int all = __all(got);
+        if (tid == 0) ok = all;
+    }
+    __syncthreads();
+    if (!ok) {
+        if (tid == 0) {
+            state->error = HMMBW_E_TIMEOUT;
+            state->done = 1;
+        }
+        return;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: nothing stale from this device's caches
+    const long long i = c * kPeerChunk + tid;
+    if (i < P.n) {
+        const double *base = reg + (long long)(seq & 1) * P.world * P.slot + i;
+        double v = 0.0;
+        for (int q = 0; q < P.world; ++q)
+            v += __hip_atomic_load(base + q * P.slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        dst[i] = v;
+    }
+}
+
 __global__ void k_init_state(IterState *st, double eps, long long max_it) {
     st->prev_L = -INFINITY;
     st->last_L = -INFINITY;
@@ -142,6 +227,8 @@ __global__ void k_init_state(IterState *st, double eps, long long max_it) {
     st->max_iterations = max_it;
     st->done = max_it <= 0 ? 1 : 0;
     st->converged = 0;
+    st->error = 0;
+    st->pad_ = 0;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -166,10 +253,11 @@ int fail(int code, const std::string &msg) {
 // hipHostFree synchronise the device and return memory to the driver: a word-sized context (20
 // utterances) spent about 1 ms in hmmbw_ctx_destroy, as long as its 30 EM iterations.  Blocks up to
 // kCacheMaxBlock bytes are rounded up to a power of two and kept per (device, kind, size) for the next
-// context, up to kCacheMaxBytes per kind and device; larger buffers go straight to the driver.
+// context, up to kCacheMaxBytes per kind and device (a word-sized context holds well under 1 MB);
+// larger buffers go straight to the driver.  hmmbw_cache_trim returns every cached block.
 // Reused blocks are not cleared: every buffer is initialised by its owner, as after hipMalloc.
 constexpr size_t kCacheMaxBlock = size_t(4) << 20;
-constexpr size_t kCacheMaxBytes = size_t(256) << 20;
+constexpr size_t kCacheMaxBytes = size_t(32) << 20;
 struct BlockCache {
     std::mutex mu;
     std::map<std::tuple<int, int, size_t>, std::vector<void *>> free;  // (device, kind, bytes) -> blocks
@@ -233,6 +321,33 @@ void cached_free(void *p, int kind) {
     }
     if (kind == kDevBlock) (void)hipFree(p);
     else (void)hipHostFree(p);
+}
+// Release every cached block (all devices); returns the bytes given back to the driver.
+size_t cache_trim() {
+    BlockCache &bc = block_cache();
+    std::vector<std::tuple<int, int, void *>> out;
+    size_t bytes = 0;
+    {
+        std::lock_guard<std::mutex> lk(bc.mu);
+        for (auto &kv : bc.free) {
+            for (void *p : kv.second) {
+                out.emplace_back(std::get<0>(kv.first), std::get<1>(kv.first), p);
+                bytes += std::get<2>(kv.first);
+                bc.size_of.erase(p);
+            }
+        }
+        bc.free.clear();
+        bc.held.clear();
+    }
+    int dev0 = 0;
+    (void)hipGetDevice(&dev0);
+    for (auto &t : out) {
+        (void)hipSetDevice(std::get<0>(t));
+        if (std::get<1>(t) == kDevBlock) (void)hipFree(std::get<2>(t));
+        else (void)hipHostFree(std::get<2>(t));
+    }
+    (void)hipSetDevice(dev0);
+    return bytes;
 }
 
 template <class T>
@@ -340,6 +455,19 @@ struct hmmbw_ctx {
     // all-reduce buffer [3][xlen] = {ncopies statistics copies, (max, sum exp) per rank}; the last
     // workgroup of each launch writes the rank's pair (d_ctr: completion counter)
     double *d_xbuf = nullptr;
+    // peer all-reduce (HMMBW_OPT_ALLREDUCE = 1): this rank's receive region, every rank's region as
+    // addressable here (attached), the IPC mappings to close, and the iteration sequence number
+    int ar_kind = HMMBW_ALLREDUCE_RCCL;
+    double *d_peer = nullptr;
+    size_t peer_bytes = 0;
+    long long peer_n = 0, peer_slot = 0, peer_nch = 0;
+    int peer_world = 0;
+    bool peer_on = false;
+    std::vector<double *> peer_regions;
+    std::vector<void *> peer_mapped;
+    unsigned long long peer_seq = 0;
+    long long peer_timeout_ms = 30000;
+    long long wall_khz = 100000;  // hipDeviceAttributeWallClockRate (100 MHz on MI355X)
     long long ar_len_last = 0;    // doubles in the last all-reduce hmmbw_iterate enqueued
     long long xlen = 0;
     int *d_ctr = nullptr;
@@ -358,6 +486,11 @@ struct hmmbw_ctx {
     std::vector<hipEvent_t> ev_free, ev_pending;  // pairs (start, stop)
     double timed_ms = 0.0;
     long long timed_n = 0;
+    // launches with a follow-up kernel (wide: k_bnum_gather): an event between the E-step kernel and
+    // it, one entry per pending pair (nullptr: none), so hmmbw_timing_split can price the E-step alone
+    std::vector<hipEvent_t> mid_free, mid_pending;
+    double timed_main_ms = 0.0;
+    long long timed_main_n = 0;
 
     long long off_S() const { return N; }
     long long off_gex() const { return N + (long long)N * N; }
@@ -373,6 +506,16 @@ struct hmmbw_ctx {
     // LDS doubles of the small kernels' tables
     size_t lds_table_doubles() const { return lds_tables() ? lds_table_bytes(K, G + kTabPad) / sizeof(double) : 0; }
     bool can_merge() const { return merge_mstep && lds_tables() && copy_len() <= kMergedMaxStats && nwaves > 0; }
+    // statistics copies in the fused all-reduce buffer: the wide path's B numerator is written once (by
+    // k_bnum_gather, into copy 0), and its tiles finish at different times, so its atomics need no
+    // spreading: one copy, and the all-reduce carries no K x N block of zeros (cfg5: 0.56 MB, not 1.1)
+    int xcopies() const { return wide ? 1 : ncopies; }
+    // doubles of the per-iteration multi-rank all-reduce: the fused buffer (copies + one (max, sum exp)
+    // pair per rank, 256-B aligned) or, in deterministic mode, the packed statistics
+    long long ar_payload() const {
+        return det ? stats_len() : ((long long)xcopies() * copy_len() + 2LL * world + 31) / 32 * 32;
+    }
+    bool peer_mode() const { return ar_kind == HMMBW_ALLREDUCE_PEER && peer_on; }
     IterState *state() const { return d_state + scur; }
     double *copies(long long e) const { return d_copies + (e % 3) * (long long)ncopies * copy_len(); }
     double *llpart(long long e) const { return d_llpart + (e % 2) * 2 * std::max(nblocks, 1LL); }
@@ -390,6 +533,14 @@ int set_device(hmmbw_ctx *c) {
 void sync_ctx(hmmbw_ctx *c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     else (void)hipDeviceSynchronize();
+}
+
+// drop the attached peer regions (closing the IPC mappings of other ranks' regions)
+void peer_detach(hmmbw_ctx *c) {
+    for (void *p : c->peer_mapped) (void)hipIpcCloseMemHandle(p);
+    c->peer_mapped.clear();
+    c->peer_regions.clear();
+    c->peer_on = false;
 }
 
 void free_obs(hmmbw_ctx *c) {
@@ -517,13 +668,26 @@ struct Plan {
 
 // E-step launch e accumulates into copies and llpart; it clears `zero` (zero_len doubles) and, when
 // `merge` is set, first runs the pending M-step in its prologue (which consumes c->pend).
+// Dense small kernels store every z_t (ZF, hmmbw_device.hpp): kChunk x the checkpoint layout.  Allocated
+// as soon as observations and a dense A are both known (set_observations / set_params), so an
+// out-of-memory surfaces there rather than in the first training call.
+int ensure_zf(hmmbw_ctx *c) {
+    if (!HMMBW_ZFULL || c->wide || !c->has_obs || !c->has_params || c->topo == HMMBW_TOPOLOGY_LEFT_TO_RIGHT || c->d_zf)
+        return HMMBW_OK;
+    if (int rc = dalloc(&c->d_zf, (size_t)std::max(c->cktot * kChunk, 1LL)))
+        return fail(rc, "dense A: the forward's every-step store (" + std::to_string(8 * c->cktot * kChunk) +
+                            " bytes) does not fit: " + g_err);
+    return HMMBW_OK;
+}
+
 int plan_estep(hmmbw_ctx *c, bool fwd_only, const IterState *state, double *copies, double *llpart, double *zero,
-               long long zero_len, bool merge, Plan *P, double *rank_ll = nullptr) {
+               long long zero_len, bool merge, Plan *P, double *rank_ll = nullptr, int ncopies = 0) {
     Plan &p = *P;
     p = Plan{};
     EArgs &a = p.a;
     a = make_eargs(c);
     a.state = state;
+    if (ncopies > 0) a.ncopies = ncopies;
     if (copies) a.copies = copies;
     if (llpart) a.llpart = llpart;
     a.zero = zero;
@@ -554,8 +718,7 @@ int plan_estep(hmmbw_ctx *c, bool fwd_only, const IterState *state, double *copi
             const size_t tabs = c->lds_table_doubles();
             p.lds = sizeof(double) * (tabs + (size_t)wpb * c->G * NV + 8);
             if (HMMBW_ZFULL && !lr && !fwd_only) {  // dense: the forward stores every z_t (hmmbw_device.hpp)
-                if (!c->d_zf)
-                    if (int rc = dalloc(&c->d_zf, (size_t)std::max(c->cktot * kChunk, 1LL))) return rc;
+                if (int rc = ensure_zf(c)) return rc;
                 a.ckpt = c->d_zf;
             }
         }
@@ -571,9 +734,9 @@ int plan_estep(hmmbw_ctx *c, bool fwd_only, const IterState *state, double *copi
 
 int launch_estep(hmmbw_ctx *c, bool fwd_only, const IterState *state, double *copies = nullptr,
                  double *llpart = nullptr, double *zero = nullptr, long long zero_len = 0, bool merge = false,
-                 double *rank_ll = nullptr) {
+                 double *rank_ll = nullptr, int ncopies = 0) {
     Plan p;
-    if (int rc = plan_estep(c, fwd_only, state, copies, llpart, zero, zero_len, merge, &p, rank_ll)) return rc;
+    if (int rc = plan_estep(c, fwd_only, state, copies, llpart, zero, zero_len, merge, &p, rank_ll, ncopies)) return rc;
     if (p.grid == 0) return HMMBW_OK;
     const EArgs &a = p.a;
     hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -590,6 +753,17 @@ int launch_estep(hmmbw_ctx *c, bool fwd_only, const IterState *state, double *co
         HIP_TRY(hipEventRecord(e0, c->stream));
     }
     if (int rc = launch_lds(p.fn, p.grid, p.lds, c->stream, a, p.block)) return rc;
+    hipEvent_t em = nullptr;
+    if (e0 && (c->wide || c->det)) {
+        if (c->mid_free.empty()) {
+            hipEvent_t x;
+            HIP_TRY(hipEventCreate(&x));
+            c->mid_free.push_back(x);
+        }
+        em = c->mid_free.back();
+        c->mid_free.pop_back();
+        HIP_TRY(hipEventRecord(em, c->stream));
+    }
     if (c->wide && !fwd_only) {  // B numerator: per-symbol gather of the gamma rows (estep_mfma.hpp)
         if (c->det) {  // deterministic mode: the other statistics from the partials, in workgroup order
             const long long n = c->off_bnum();
@@ -612,6 +786,7 @@ int launch_estep(hmmbw_ctx *c, bool fwd_only, const IterState *state, double *co
         HIP_TRY(hipEventRecord(e1, c->stream));
         c->ev_pending.push_back(e0);
         c->ev_pending.push_back(e1);
+        c->mid_pending.push_back(em);
     }
     return HMMBW_OK;
 }
@@ -623,10 +798,17 @@ int drain_timing(hmmbw_ctx *c) {
         HIP_TRY(hipEventElapsedTime(&ms, c->ev_pending[i], c->ev_pending[i + 1]));
         c->timed_ms += ms;
         c->timed_n += 1;
+        if (hipEvent_t em = c->mid_pending[i / 2]) {
+            HIP_TRY(hipEventElapsedTime(&ms, c->ev_pending[i], em));
+            c->timed_main_ms += ms;
+            c->timed_main_n += 1;
+            c->mid_free.push_back(em);
+        }
         c->ev_free.push_back(c->ev_pending[i]);
         c->ev_free.push_back(c->ev_pending[i + 1]);
     }
     c->ev_pending.clear();
+    c->mid_pending.clear();
     return HMMBW_OK;
 }
 
@@ -734,6 +916,12 @@ int hmmbw_device_count(int *out) {
     return HMMBW_OK;
 }
 
+int hmmbw_cache_trim(int64_t *bytes_released) {
+    const size_t b = cache_trim();
+    if (bytes_released) *bytes_released = (int64_t)b;
+    return HMMBW_OK;
+}
+
 int hmmbw_ctx_create(int device, int n_states, int n_symbols, hmmbw_ctx **out) {
     if (!out) return fail(HMMBW_E_INVALID, "null out");
     *out = nullptr;
@@ -750,6 +938,11 @@ int hmmbw_ctx_create(int device, int n_states, int n_symbols, hmmbw_ctx **out) {
     c->G = c->wide ? c->NP : (n_states <= 2 ? 2 : n_states <= 4 ? 4 : n_states <= 8 ? 8 : 16);
     c->U = c->wide ? 16 : kWave / c->G;
     int rc = set_device(c);
+    if (!rc) {
+        int khz = 0;
+        if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) == hipSuccess && khz > 0)
+            c->wall_khz = khz;
+    }
     if (!rc) rc = dalloc(&c->d_pi, c->N);
     if (!rc) rc = dalloc(&c->d_A, (size_t)c->N * c->N);
     if (!rc) rc = dalloc(&c->d_B, (size_t)c->N * c->K);
@@ -780,8 +973,10 @@ int hmmbw_ctx_create(int device, int n_states, int n_symbols, hmmbw_ctx **out) {
 int hmmbw_ctx_destroy(hmmbw_ctx *c) {
     if (!c) return HMMBW_OK;
     (void)hipSetDevice(c->device);
-    if (c->stream) (void)hipStreamSynchronize(c->stream);
-    else (void)hipDeviceSynchronize();
+    // the whole device, not just the context stream: a caller may still use a buffer the context
+    // handed out (hmmbw_iterate_begin) on its own stream, and the block cache reuses freed blocks at
+    // once (hipFree used to synchronise the device implicitly)
+    (void)hipDeviceSynchronize();
     dfree(c->d_pi); dfree(c->d_A); dfree(c->d_B); dfree(c->d_Bt); dfree(c->d_out);
     for (auto &sn : c->snaps) {
         if (sn.ev) (void)hipEventDestroy(sn.ev);
@@ -794,9 +989,15 @@ int hmmbw_ctx_destroy(hmmbw_ctx *c) {
         if (rccl_load(nullptr, &r) == HMMBW_OK) (void)r->comm_destroy(c->comm);
         c->comm = nullptr;
     }
+    peer_detach(c);
+    if (c->d_peer) (void)hipFree(c->d_peer);  // its own allocation (IPC-exported), not the block cache
+    c->d_peer = nullptr;
     free_obs(c);
     for (auto e : c->ev_free) (void)hipEventDestroy(e);
     for (auto e : c->ev_pending) (void)hipEventDestroy(e);
+    for (auto e : c->mid_free) (void)hipEventDestroy(e);
+    for (auto e : c->mid_pending)
+        if (e) (void)hipEventDestroy(e);
     for (auto e : c->ar_free) (void)hipEventDestroy(e);
     for (auto e : c->ar_pending) (void)hipEventDestroy(e);
     delete c;
@@ -805,7 +1006,16 @@ int hmmbw_ctx_destroy(hmmbw_ctx *c) {
 
 int hmmbw_set_stream(hmmbw_ctx *c, void *stream) {
     if (!c) return fail(HMMBW_E_INVALID, "null context");
-    c->stream = reinterpret_cast<hipStream_t>(stream);
+    if (c->ar_open) return fail(HMMBW_E_STATE, "an iteration is open (hmmbw_iterate_end first)");
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if (s != c->stream) {
+        // later frees synchronise only the NEW stream: the block cache must not hand a buffer that work
+        // queued on the old one still uses to another context
+        if (int rc = set_device(c)) return rc;
+        if (c->stream) HIP_TRY(hipStreamSynchronize(c->stream));
+        else HIP_TRY(hipDeviceSynchronize());
+    }
+    c->stream = s;
     return HMMBW_OK;
 }
 
@@ -815,6 +1025,7 @@ int hmmbw_set_rank(hmmbw_ctx *c, int rank, int world) {
     if (world < 1 || rank < 0 || rank >= world) return fail(HMMBW_E_INVALID, "bad rank/world");
     if (int rc = set_device(c)) return rc;
     if (int rc = flush_mstep(c)) return rc;
+    if (c->rank != rank || c->world != world) peer_detach(c);  // the regions are sized for the old world
     c->rank = rank;
     c->world = world;
     return realloc_stats(c);
@@ -1022,7 +1233,7 @@ int hmmbw_set_observations(hmmbw_ctx *c, const int64_t *offsets, const int32_t *
     c->nfull = nfull;
     c->xact = xact;
     c->has_obs = true;
-    return HMMBW_OK;
+    return ensure_zf(c);
 }
 
 int hmmbw_set_option(hmmbw_ctx *c, int key, int64_t value) {
@@ -1051,6 +1262,17 @@ int hmmbw_set_option(hmmbw_ctx *c, int key, int64_t value) {
         if (int rc = set_device(c)) return rc;
         if (int rc = flush_mstep(c)) return rc;
         c->merge_mstep = value != 0;
+        return HMMBW_OK;
+    }
+    if (key == HMMBW_OPT_ALLREDUCE) {
+        if (value != HMMBW_ALLREDUCE_RCCL && value != HMMBW_ALLREDUCE_PEER)
+            return fail(HMMBW_E_INVALID, "HMMBW_OPT_ALLREDUCE: 0 (RCCL / caller) or 1 (peer)");
+        c->ar_kind = (int)value;
+        return HMMBW_OK;
+    }
+    if (key == HMMBW_OPT_PEER_TIMEOUT_MS) {
+        if (value < 1) return fail(HMMBW_E_INVALID, "peer timeout must be >= 1 ms");
+        c->peer_timeout_ms = value;
         return HMMBW_OK;
     }
     if (key == HMMBW_OPT_ABLATE) {  // diagnostics: results are wrong while set
@@ -1085,7 +1307,7 @@ int hmmbw_set_params(hmmbw_ctx *c, const double *pi, const double *A, const doub
     c->h_A = hA;
     c->has_params = true;
     resolve_topology(c);
-    return HMMBW_OK;
+    return ensure_zf(c);
 }
 
 int hmmbw_reset_training(hmmbw_ctx *c, double epsilon, int64_t max_iterations) {
@@ -1156,10 +1378,12 @@ static int mr_begin(hmmbw_ctx *c, long long n_seq_global, double **buf, long lon
     if (fused) {
         // rounded to 256 B so all three buffers keep the copies' alignment (a 16-B shift splits the
         // B-numerator rows' 64-B segments over two cache lines; ~0.7 us per launch at cfg3)
-        const long long xl = ((long long)c->ncopies * c->copy_len() + 2LL * c->world + 31) / 32 * 32;
+        const int nc = c->xcopies();
+        const long long xl = c->ar_payload();
         if (c->xlen != xl) {
             if (int rc = flush_mstep(c)) return rc;
-            HIP_TRY(hipStreamSynchronize(c->stream));
+            // the caller may still read or write the old buffer on its own stream (its all-reduce)
+            HIP_TRY(hipDeviceSynchronize());
             dfree(c->d_xbuf);
             if (int rc = dalloc(&c->d_xbuf, 3 * (size_t)xl)) return rc;
             HIP_TRY(hipMemsetAsync(c->d_xbuf, 0, sizeof(double) * 3 * (size_t)xl, c->stream));
@@ -1170,11 +1394,11 @@ static int mr_begin(hmmbw_ctx *c, long long n_seq_global, double **buf, long lon
             if (int rc = flush_mstep(c)) return rc;
         const long long e = c->e_count++;
         double *X = c->d_xbuf + (e % 3) * c->xlen, *Xn = c->d_xbuf + ((e + 1) % 3) * c->xlen;
-        const long long ll_off = (long long)c->ncopies * c->copy_len();
+        const long long ll_off = (long long)nc * c->copy_len();
         // accumulate into X (the merged M-step reads the previous, all-reduced X), clear the next
         if (c->nblocks > 0) {
             if (int rc = launch_estep(c, false, c->state(), X, c->llpart(e), Xn, c->xlen, true,
-                                      X + ll_off + 2LL * c->rank))
+                                      X + ll_off + 2LL * c->rank, nc))
                 return rc;
         } else {  // empty shard: contribute zeros (no E-step launch clears the buffers)
             HIP_TRY(hipMemsetAsync(X, 0, sizeof(double) * (size_t)c->xlen, c->stream));
@@ -1201,6 +1425,38 @@ static int mr_begin(hmmbw_ctx *c, long long n_seq_global, double **buf, long lon
     return HMMBW_OK;
 }
 
+// Peer all-reduce halves (kernels above): push this rank's buffer to every rank's slot `rank` after the
+// E-step, and wait for / sum every rank's slot before the M-step.
+static PeerArgs peer_args(const hmmbw_ctx *c) {
+    PeerArgs P{};
+    for (int r = 0; r < c->peer_world; ++r) P.region[r] = c->peer_regions[(size_t)r];
+    P.n = c->peer_n;
+    P.slot = c->peer_slot;
+    P.nch = c->peer_nch;
+    P.world = c->peer_world;
+    P.rank = c->rank;
+    return P;
+}
+
+static int peer_push(hmmbw_ctx *c, const double *buf, long long len) {
+    if (len != c->peer_n || c->peer_world != c->world)
+        return fail(HMMBW_E_STATE, "the all-reduce payload changed after hmmbw_peer_region (rank, world or options "
+                                   "set after it): set up the peer regions again");
+    c->peer_seq += 1;
+    hipLaunchKernelGGL(k_peer_push, dim3((unsigned)c->peer_nch, (unsigned)c->peer_world), dim3(kPeerChunk), 0,
+                       c->stream, buf, peer_args(c), c->peer_seq, c->state());
+    HIP_TRY(hipGetLastError());
+    return HMMBW_OK;
+}
+
+static int peer_reduce(hmmbw_ctx *c, double *buf) {
+    const long long ticks = std::max(1LL, c->peer_timeout_ms) * c->wall_khz;
+    hipLaunchKernelGGL(k_peer_reduce, dim3((unsigned)c->peer_nch), dim3(kPeerChunk), 0, c->stream, buf, peer_args(c),
+                       c->peer_seq, c->state(), ticks);
+    HIP_TRY(hipGetLastError());
+    return HMMBW_OK;
+}
+
 // Second half: the M-step from the all-reduced buffer (merged into the next E-step launch when it can).
 static int mr_end(hmmbw_ctx *c) {
     if (!c->ar_open) return fail(HMMBW_E_STATE, "no open iteration (hmmbw_iterate_begin first)");
@@ -1210,8 +1466,8 @@ static int mr_end(hmmbw_ctx *c) {
     p.on = true;
     p.local = false;
     p.src = c->ar_cur;
-    p.nsrc = c->ncopies;
-    p.ll = c->ar_cur + (long long)c->ncopies * c->copy_len();
+    p.nsrc = c->xcopies();
+    p.ll = c->ar_cur + (long long)c->xcopies() * c->copy_len();
     p.nll = c->world;
     p.ext = c->ar_cur;
     p.R = c->ar_R;
@@ -1222,49 +1478,184 @@ int hmmbw_iterate_begin(hmmbw_ctx *c, int64_t n_seq_global, double **buf, int64_
     if (int rc = check_ready(c, true)) return rc;
     if (!buf || !n_doubles) return fail(HMMBW_E_INVALID, "null argument");
     if (n_seq_global < 0) return fail(HMMBW_E_INVALID, "negative sequence count");
+    if (c->ar_kind == HMMBW_ALLREDUCE_PEER && !c->peer_on)
+        return fail(HMMBW_E_STATE, "peer all-reduce selected but no regions attached (hmmbw_peer_open / _attach)");
     long long len = 0;
     if (int rc = mr_begin(c, n_seq_global, buf, &len)) return rc;
+    if (c->peer_mode()) {  // the whole exchange is the engine's: push now, wait + sum in _end
+        if (int rc = peer_push(c, *buf, len)) {
+            c->ar_open = false;
+            return rc;
+        }
+        c->ar_len_last = len;
+    }
     *n_doubles = len;
     return HMMBW_OK;
 }
 
 int hmmbw_iterate_end(hmmbw_ctx *c) {
     if (int rc = check_ready(c, true)) return rc;
+    if (c->ar_open && c->peer_mode())
+        if (int rc = peer_reduce(c, c->ar_cur)) {
+            c->ar_open = false;
+            return rc;
+        }
     return mr_end(c);
+}
+
+int hmmbw_peer_region(hmmbw_ctx *c, void **region, int64_t *bytes) {
+    if (!c || !region || !bytes) return fail(HMMBW_E_INVALID, "null argument");
+    if (c->ar_open) return fail(HMMBW_E_STATE, "an iteration is open (hmmbw_iterate_end first)");
+    if (c->world > kMaxPeers) return fail(HMMBW_E_UNSUPPORTED, "peer all-reduce: at most 16 ranks");
+    if (int rc = set_device(c)) return rc;
+    const long long n = c->ar_payload();
+    const long long slot = (n + 31) / 32 * 32, nch = (n + kPeerChunk - 1) / kPeerChunk;
+    const size_t b = sizeof(double) * 2 * (size_t)c->world * (size_t)slot +
+                     sizeof(unsigned long long) * (size_t)c->world * (size_t)nch;
+    if (!c->d_peer || c->peer_n != n || c->peer_world != c->world) {
+        peer_detach(c);
+        HIP_TRY(hipDeviceSynchronize());
+        if (c->d_peer) HIP_TRY(hipFree(c->d_peer));
+        c->d_peer = nullptr;
+        // its own allocation (exported with hipIpcGetMemHandle), never a block of the cache
+        HIP_TRY(hipMalloc(reinterpret_cast<void **>(&c->d_peer), b));
+        HIP_TRY(hipMemset(c->d_peer, 0, b));
+        c->peer_bytes = b;
+        c->peer_n = n;
+        c->peer_slot = slot;
+        c->peer_nch = nch;
+        c->peer_world = c->world;
+    }
+    *region = c->d_peer;
+    *bytes = (int64_t)c->peer_bytes;
+    return HMMBW_OK;
+}
+
+int hmmbw_peer_ipc_handle(hmmbw_ctx *c, void *handle_out) {
+    if (!c || !handle_out) return fail(HMMBW_E_INVALID, "null argument");
+    if (!c->d_peer) return fail(HMMBW_E_STATE, "no peer region (hmmbw_peer_region first)");
+    if (int rc = set_device(c)) return rc;
+    hipIpcMemHandle_t h;
+    HIP_TRY(hipIpcGetMemHandle(&h, c->d_peer));
+    static_assert(sizeof(h) == 64, "HIP IPC handles are 64 bytes");
+    std::memcpy(handle_out, &h, sizeof(h));
+    return HMMBW_OK;
+}
+
+static int peer_attach_impl(hmmbw_ctx *c, const std::vector<double *> &regions, int64_t n_seq_global) {
+    HIP_TRY(hipDeviceSynchronize());
+    // a fresh exchange: clear this rank's slots and flags (every rank attaches before any iterates)
+    HIP_TRY(hipMemset(c->d_peer, 0, c->peer_bytes));
+    c->peer_regions = regions;
+    c->peer_seq = 0;
+    c->peer_on = true;
+    c->R_global = n_seq_global;  // the R of hmm_training.py:424 for hmmbw_iterate's loop
+    return HMMBW_OK;
+}
+
+int hmmbw_peer_attach(hmmbw_ctx *c, void *const *regions, int64_t n_seq_global) {
+    if (!c || !regions) return fail(HMMBW_E_INVALID, "null argument");
+    if (n_seq_global < 0) return fail(HMMBW_E_INVALID, "negative sequence count");
+    if (c->ar_open) return fail(HMMBW_E_STATE, "an iteration is open (hmmbw_iterate_end first)");
+    if (!c->d_peer || c->peer_world != c->world || c->peer_n != c->ar_payload())
+        return fail(HMMBW_E_STATE, "no current peer region (hmmbw_peer_region first, after set_rank and options)");
+    if (regions[c->rank] != c->d_peer) return fail(HMMBW_E_INVALID, "regions[rank] must be this context's own region");
+    std::vector<double *> reg((size_t)c->world);
+    for (int r = 0; r < c->world; ++r) {
+        if (!regions[r]) return fail(HMMBW_E_INVALID, "null peer region");
+        reg[(size_t)r] = static_cast<double *>(regions[r]);
+    }
+    if (int rc = set_device(c)) return rc;
+    peer_detach(c);
+    return peer_attach_impl(c, reg, n_seq_global);
+}
+
+int hmmbw_peer_open(hmmbw_ctx *c, const void *handles, int64_t n_seq_global) {
+    if (!c || !handles) return fail(HMMBW_E_INVALID, "null argument");
+    if (n_seq_global < 0) return fail(HMMBW_E_INVALID, "negative sequence count");
+    if (c->ar_open) return fail(HMMBW_E_STATE, "an iteration is open (hmmbw_iterate_end first)");
+    if (!c->d_peer || c->peer_world != c->world || c->peer_n != c->ar_payload())
+        return fail(HMMBW_E_STATE, "no current peer region (hmmbw_peer_region first, after set_rank and options)");
+    if (int rc = set_device(c)) return rc;
+    peer_detach(c);
+    std::vector<double *> reg((size_t)c->world, nullptr);
+    const char *hb = static_cast<const char *>(handles);
+    for (int r = 0; r < c->world; ++r) {
+        if (r == c->rank) {
+            reg[(size_t)r] = c->d_peer;
+            continue;
+        }
+        hipIpcMemHandle_t h;
+        std::memcpy(&h, hb + 64 * (size_t)r, sizeof(h));
+        void *p = nullptr;
+        const hipError_t e = hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess);
+        if (e != hipSuccess) {
+            peer_detach(c);
+            return fail(HMMBW_E_HIP, "hipIpcOpenMemHandle (rank " + std::to_string(r) + "): " + hipGetErrorString(e));
+        }
+        c->peer_mapped.push_back(p);
+        reg[(size_t)r] = static_cast<double *>(p);
+    }
+    return peer_attach_impl(c, reg, n_seq_global);
+}
+
+int hmmbw_allreduce_kind(const hmmbw_ctx *c, int *kind) {
+    if (!c || !kind) return fail(HMMBW_E_INVALID, "null argument");
+    if (c->peer_mode()) *kind = HMMBW_ALLREDUCE_PEER;
+    else if (c->world > 1 || c->comm) *kind = HMMBW_ALLREDUCE_RCCL;
+    else *kind = -1;
+    return HMMBW_OK;
 }
 
 int hmmbw_iterate(hmmbw_ctx *c, int64_t n_iter) {
     if (int rc = check_ready(c, true)) return rc;
     if (c->ar_open) return fail(HMMBW_E_STATE, "an iteration is open (hmmbw_iterate_end first)");
-    if (c->world != 1 || c->comm) {
-        // multi-rank with the native communicator: estep -> ncclAllReduce (this stream) -> mstep
-        if (!c->comm) return fail(HMMBW_E_STATE, "multi-rank hmmbw_iterate needs hmmbw_comm_init "
-                                                 "(or use hmmbw_iterate_begin / all-reduce / _end)");
+    if (c->world != 1 || c->comm || c->peer_mode()) {
+        // multi-rank with the engine's own all-reduce: estep -> ncclAllReduce (this stream) or the peer
+        // push / wait + sum -> mstep
+        const bool peer = c->peer_mode();
+        if (c->ar_kind == HMMBW_ALLREDUCE_PEER && !peer)
+            return fail(HMMBW_E_STATE, "peer all-reduce selected but no regions attached (hmmbw_peer_open / _attach)");
+        if (!peer && !c->comm)
+            return fail(HMMBW_E_STATE, "multi-rank hmmbw_iterate needs hmmbw_comm_init or the peer all-reduce "
+                                       "(or use hmmbw_iterate_begin / all-reduce / _end)");
         Rccl *r = nullptr;
-        if (int rc = rccl_load(nullptr, &r)) return rc;
+        if (!peer)
+            if (int rc = rccl_load(nullptr, &r)) return rc;
         for (int64_t i = 0; i < n_iter; ++i) {
             double *ar = nullptr;
             long long ar_len = 0;
             if (int rc = mr_begin(c, c->R_global, &ar, &ar_len)) return rc;
-            hipEvent_t e0 = nullptr, e1 = nullptr;
-            if (c->timing && (c->ar_seq++ % c->timing) == 0) {
-                if (int rc = take_events(c->ar_free, &e0, &e1)) return rc;
-                HIP_TRY(hipEventRecord(e0, c->stream));
-            }
-            // also at world 1 (RCCL's in-place 1-rank sum is a copy kernel, ~2 us): the 1-rank
-            // communicator tests then exercise the same ncclAllReduce call as an 8-GPU run
-            c->ar_len_last = ar_len;
-            ncclResult_t e = r->all_reduce(ar, ar, (size_t)ar_len, ncclFloat64, ncclSum, c->comm, c->stream);
-            if (e != ncclSuccess) {
+            // between mr_begin and mr_end: any failure closes the iteration again, or every later
+            // training call would fail with HMMBW_E_STATE
+            auto collective = [&]() -> int {
+                hipEvent_t e0 = nullptr, e1 = nullptr;
+                if (c->timing && (c->ar_seq++ % c->timing) == 0) {
+                    if (int rc = take_events(c->ar_free, &e0, &e1)) return rc;
+                    HIP_TRY(hipEventRecord(e0, c->stream));
+                }
+                // also at world 1 (RCCL's in-place 1-rank sum is a copy kernel, ~2 us): the 1-rank
+                // communicator tests then exercise the same ncclAllReduce call as an 8-GPU run
+                c->ar_len_last = ar_len;
+                if (peer) {
+                    if (int rc = peer_push(c, ar, ar_len)) return rc;
+                    if (int rc = peer_reduce(c, ar)) return rc;
+                } else {
+                    ncclResult_t e = r->all_reduce(ar, ar, (size_t)ar_len, ncclFloat64, ncclSum, c->comm, c->stream);
+                    if (e != ncclSuccess) return rccl_fail(r, e, "ncclAllReduce");
+                }
+                if (e1) {
+                    HIP_TRY(hipEventRecord(e1, c->stream));
+                    c->ar_pending.push_back(e0);
+                    c->ar_pending.push_back(e1);
+                    if (c->ar_pending.size() >= 256)
+                        if (int rc = drain_pairs(c->ar_pending, c->ar_free, &c->ar_ms, &c->ar_n)) return rc;
+                }
+                return HMMBW_OK;
+            };
+            if (int rc = collective()) {
                 c->ar_open = false;
-                return rccl_fail(r, e, "ncclAllReduce");
-            }
-            if (e1) {
-                HIP_TRY(hipEventRecord(e1, c->stream));
-                c->ar_pending.push_back(e0);
-                c->ar_pending.push_back(e1);
-                if (c->ar_pending.size() >= 256)
-                    if (int rc = drain_pairs(c->ar_pending, c->ar_free, &c->ar_ms, &c->ar_n)) return rc;
+                return rc;
             }
             if (int rc = mr_end(c)) return rc;
         }
@@ -1315,6 +1706,8 @@ int hmmbw_get_status(hmmbw_ctx *c, hmmbw_status *st, hmmbw_iter_record *rec, int
         HIP_TRY(hipMemcpyAsync(hist.data(), c->d_hist, sizeof(double) * hist.size(), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     fill_status(h, st);
+    if (h.error) return fail(h.error, "EM stopped on a device-side failure: a rank did not deliver its statistics to "
+                                      "the peer all-reduce within HMMBW_OPT_PEER_TIMEOUT_MS");
     if (rec && count > 0) {
         if (first < 0 || first + count > h.iteration || first < h.iteration - kHist)
             return fail(HMMBW_E_INVALID, "requested iteration records are not available");
@@ -1362,6 +1755,8 @@ int hmmbw_status_wait(hmmbw_ctx *c, int64_t ticket, hmmbw_status *st, hmmbw_iter
     HIP_TRY(hipEventSynchronize(sn.ev));  // this snapshot only, not the work enqueued after it
     const IterState h = *sn.st;
     fill_status(h, st);
+    if (h.error) return fail(h.error, "EM stopped on a device-side failure: a rank did not deliver its statistics to "
+                                      "the peer all-reduce within HMMBW_OPT_PEER_TIMEOUT_MS");
     if (rec && count > 0) {
         if (first < sn.first || first + count > h.iteration || first + count > sn.first + kHist ||
             first < h.iteration - kHist)  // overwritten in the ring before the snapshot was taken
@@ -1409,6 +1804,7 @@ int hmmbw_get_loglik(hmmbw_ctx *c, double *out) {
 int hmmbw_score(hmmbw_ctx *c, double *out) {
     if (int rc = check_ready(c, false)) return rc;
     if (!out) return fail(HMMBW_E_INVALID, "null argument");
+    if (c->ar_open) return fail(HMMBW_E_STATE, "an iteration is open (hmmbw_iterate_end first)");
     if (int rc = flush_mstep(c)) return rc;
     if (int rc = launch_estep(c, true, nullptr)) return rc;
     return hmmbw_get_loglik(c, out);
@@ -1425,7 +1821,18 @@ int hmmbw_timing(hmmbw_ctx *c, int enable, double *total_ms, int64_t *count) {
         c->timing_seq = 0;
         c->timed_ms = 0.0;
         c->timed_n = 0;
+        c->timed_main_ms = 0.0;
+        c->timed_main_n = 0;
     }
+    return HMMBW_OK;
+}
+
+int hmmbw_timing_split(hmmbw_ctx *c, double *main_ms, int64_t *count) {
+    if (!c) return fail(HMMBW_E_INVALID, "null context");
+    if (int rc = set_device(c)) return rc;
+    if (int rc = drain_timing(c)) return rc;
+    if (main_ms) *main_ms = c->timed_main_ms;
+    if (count) *count = c->timed_main_n;
     return HMMBW_OK;
 }
 
@@ -1464,6 +1871,7 @@ int group_check(hmmbw_group *g, bool need_armed) {
     for (hmmbw_ctx *c : g->m) {
         if (int rc = check_ready(c, need_armed)) return rc;
         if (c->world != 1) return fail(HMMBW_E_STATE, "group members are single-rank contexts");
+        if (c->ar_open) return fail(HMMBW_E_STATE, "a group member has an open iteration (hmmbw_iterate_end first)");
         if (c->device != c0->device || c->stream != c0->stream)
             return fail(HMMBW_E_INVALID, "group members must share the device and the stream");
         if (c->N != c0->N || c->K != c0->K || c->topo != c0->topo || c->wide || !c->lds_tables())

@@ -80,6 +80,8 @@ struct IterState {
     long long max_iterations;
     int done;
     int converged;
+    int error;  // HMMBW_E_* of a device-side failure (peer all-reduce timeout); done is set with it
+    int pad_;
 };
 
 // Observation layout in HBM (built once by hmmbw_set_observations).
@@ -629,9 +631,10 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
                         C += st;
                     }
                     sp[k] = st;
-                    if constexpr (!FWD_ONLY)
+                    if constexpr (!FWD_ONLY) {
                         if (ZF) ckw[((long long)c * kChunk + k) * kWave] = z;  // every z_t
                         else if (k == 0) ckw[(long long)c * kWave] = z;    // checkpoint z_{8c}
+                    }
                 }
                 if constexpr (!FWD_ONLY) spw[(long long)c * U] = pack_exps(sp);
             };
@@ -1531,6 +1534,7 @@ __device__ bool merged_mstep(const EArgs &a, double *sP, double *sH, double *sPA
         in.max_iterations = m.state->max_iterations;
         in.done = m.state->done;
         in.converged = m.state->converged;
+        in.error = m.state->error;
         in.last_L = m.state->last_L;
         in.last_diff = m.state->last_diff;
     }

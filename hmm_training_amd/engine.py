@@ -25,7 +25,8 @@ from typing import Callable, List, Optional, Sequence, Tuple
 import numpy as np
 import torch
 
-from ._lib import OPT_DETERMINISTIC, OPT_MERGE_MSTEP, OPT_SAFE_SCALING, OPT_STAT_COPIES, TOPOLOGY, TOPOLOGY_NAME, IterRecord, Status, check, lib
+from ._lib import (ALLREDUCE, OPT_ALLREDUCE, OPT_DETERMINISTIC, OPT_MERGE_MSTEP, OPT_PEER_TIMEOUT_MS, OPT_SAFE_SCALING,
+                   OPT_STAT_COPIES, TOPOLOGY, TOPOLOGY_NAME, IterRecord, Status, check, lib)
 
 IterCallback = Callable[[int, float, float], None]
 
@@ -113,7 +114,7 @@ class BaumWelchEngine:
     def __init__(self, n_states: int, n_symbols: int, device: Optional[int] = None, topology: str = "auto",
                  rank: int = 0, world_size: int = 1, stream: Optional[int] = None, safe_scaling: bool = False,
                  merge_mstep: bool = True, stat_copies: Optional[int] = None, group=None, native_comm: Optional[bool] = None,
-                 deterministic: bool = False):
+                 deterministic: bool = False, allreduce: Optional[str] = None, peer_timeout_ms: Optional[int] = None):
         self._lib = lib()
         self.N, self.M = int(n_states), int(n_symbols)
         self.device = default_device() if device is None else int(device)
@@ -144,6 +145,16 @@ class BaumWelchEngine:
         if native_comm is None:
             native_comm = os.environ.get("HMMBW_NATIVE_COMM", "1") != "0"
         self._want_native = bool(native_comm) and self.world_size > 1
+        # multi-rank all-reduce of the engine's own loop: "rccl" (engine communicator), "peer" (the engine's
+        # push / wait + sum over IPC-mapped receive regions, hmmbw_peer_*), or "both" (set up both, RCCL
+        # active; set_allreduce switches between iterations)
+        self.allreduce_req = (allreduce or os.environ.get("HMMBW_ALLREDUCE", "rccl")).lower()
+        if self.allreduce_req not in ("rccl", "peer", "both"):
+            raise ValueError(f"allreduce must be rccl, peer or both, not {self.allreduce_req!r}")
+        self._rccl_ok = False
+        self._peer_ok = False
+        if peer_timeout_ms is not None:
+            check(self._lib.hmmbw_set_option(self._ctx, OPT_PEER_TIMEOUT_MS, int(peer_timeout_ms)))
         self._timing_mode = 0  # hmmbw_timing mode last set through timing()
 
     # -------------------------------------------------------------------------------- set-up
@@ -159,8 +170,61 @@ class BaumWelchEngine:
         self.n_symbols_total = int(offsets[-1]) if R > 0 else 0
         self.n_seq_global = R if n_seq_global is None else int(n_seq_global)
         if self._want_native and self._native_R != self.n_seq_global:
-            self._native = self._init_native_comm()
+            want_rccl = self.allreduce_req in ("rccl", "both")
+            want_peer = self.allreduce_req in ("peer", "both")
+            self._rccl_ok = self._init_native_comm() if want_rccl else False
+            self._peer_ok = self._init_peer() if want_peer else False
+            if self._rccl_ok and self.allreduce_req != "peer":
+                self.set_allreduce("rccl")
+            elif self._peer_ok:
+                self.set_allreduce("peer")
+            self._native = self._rccl_ok or self._peer_ok
             self._native_R = self.n_seq_global if self._native else None
+
+    def set_allreduce(self, kind: str) -> None:
+        """Switch the engine loop's all-reduce between iterations: "rccl" or "peer" (each must be set up)."""
+        if kind == "rccl" and not self._rccl_ok:
+            raise RuntimeError("the RCCL engine communicator is not set up")
+        if kind == "peer" and not self._peer_ok:
+            raise RuntimeError("the peer all-reduce is not set up")
+        check(self._lib.hmmbw_set_option(self._ctx, OPT_ALLREDUCE, ALLREDUCE[kind]))
+
+    @property
+    def allreduce(self) -> Optional[str]:
+        """The all-reduce the engine loop uses now: "rccl", "peer", or None (single rank / torch hop)."""
+        k = ctypes.c_int()
+        check(self._lib.hmmbw_allreduce_kind(self._ctx, ctypes.byref(k)))
+        if k.value == ALLREDUCE["peer"]:
+            return "peer"
+        return "rccl" if (k.value == ALLREDUCE["rccl"] and self._native) else None
+
+    def _agree(self, ok: bool) -> bool:
+        """True iff every rank passes ok (an all-reduce MIN on the process group's device)."""
+        import torch.distributed as dist
+        dev = f"cuda:{self.device}" if dist.get_backend(self._group) == "nccl" else "cpu"
+        flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self._group)
+        return int(flag.item()) == 1
+
+    def _init_peer(self) -> bool:
+        """Collective over the ranks: the peer all-reduce (include/hmmbw.h, hmmbw_peer_*).  Every rank
+        allocates its receive region, the 64-byte IPC handles are all-gathered over the process group (any
+        backend), and every rank maps the others' regions; used only if every rank succeeded."""
+        import torch.distributed as dist
+        if not (dist.is_available() and dist.is_initialized()):
+            return False
+        region, nbytes = ctypes.c_void_p(), ctypes.c_int64()
+        handle = ctypes.create_string_buffer(64)
+        ok = (self._lib.hmmbw_peer_region(self._ctx, ctypes.byref(region), ctypes.byref(nbytes)) == 0 and
+              self._lib.hmmbw_peer_ipc_handle(self._ctx, handle) == 0)
+        if not self._agree(ok):
+            return False
+        handles = [None] * dist.get_world_size(self._group)
+        dist.all_gather_object(handles, handle.raw, group=self._group)
+        buf = ctypes.create_string_buffer(b"".join(handles), 64 * len(handles))
+        rc = self._lib.hmmbw_peer_open(self._ctx, buf, self.n_seq_global)
+        # every rank must have attached (cleared its flags) before any rank pushes
+        return self._agree(rc == 0)
 
     def _init_native_comm(self) -> bool:
         """Collective over the ranks: give the context its own RCCL communicator (hmmbw_comm_init), so
@@ -388,6 +452,14 @@ class BaumWelchEngine:
         ms = ctypes.c_double()
         n = ctypes.c_int64()
         check(self._lib.hmmbw_timing(self._ctx, int(enable), ctypes.byref(ms), ctypes.byref(n)))
+        return ms.value, n.value
+
+    def timing_split(self) -> Tuple[float, int]:
+        """(E-step kernel ms, count) of the timed launches that run a follow-up kernel after the E-step
+        kernel (wide path: k_bnum_gather) -- hmmbw_timing_split; same reset as timing()."""
+        ms = ctypes.c_double()
+        n = ctypes.c_int64()
+        check(self._lib.hmmbw_timing_split(self._ctx, ctypes.byref(ms), ctypes.byref(n)))
         return ms.value, n.value
 
     def comm_info(self, reset: bool = False) -> Tuple[int, float, int]:

@@ -32,7 +32,8 @@
 extern "C" {
 #endif
 
-#define HMMBW_ABI_VERSION 2 /* 2: hmmbw_iterate_begin/_end, status snapshots, comm info/payload */
+#define HMMBW_ABI_VERSION 3 /* 2: hmmbw_iterate_begin/_end, status snapshots, comm info/payload;
+                              3: peer all-reduce (hmmbw_peer_*), HMMBW_E_TIMEOUT, cache trim, split timing */
 
 #define HMMBW_OK 0
 #define HMMBW_E_INVALID (-1)        /* bad argument (shape, range, null pointer)             */
@@ -42,6 +43,8 @@ extern "C" {
 #define HMMBW_E_EMPTY_SEQUENCE (-5) /* a sequence of length 0: the reference raises IndexError
                                        at hmm_training.py:376 / hmm_testing.py:75              */
 #define HMMBW_E_SYMBOL_RANGE (-6)   /* symbol id >= M: numpy IndexError at hmm_training.py:360 */
+#define HMMBW_E_TIMEOUT (-7)        /* a rank did not deliver its statistics to the peer all-reduce in time
+                                       (bounded device-side wait; EM stops, status calls report it)  */
 
 /* Transition-matrix kernel variant (the reference skips -inf transitions,
  * hmm_training.py:143-144,186-188; a left-to-right A keeps its zero pattern under EM). */
@@ -69,6 +72,14 @@ typedef struct {
 int hmmbw_abi_version(void);
 const char *hmmbw_last_error(void);
 int hmmbw_device_count(int *out);
+
+/* The library keeps the small device buffers and pinned snapshot blocks of destroyed contexts (blocks
+ * <= 4 MB, at most 32 MB per kind and device) for the next context: the drop-in builds one context per
+ * hmm_training call (hmm_training.py:265-267) and hipFree synchronises the device.  This returns every
+ * cached block to the driver (e.g. before a memory-hungry phase of the process, or on an
+ * out-of-memory); *bytes_released (may be NULL) gets the total.  Blocks of live contexts are not
+ * touched. */
+int hmmbw_cache_trim(int64_t *bytes_released);
 
 /* Context for one (device, N states, M symbols) model.  Replaces the parameter set-up of
  * hmm_training.py:268-339 (allocation is sized by hmmbw_set_observations). */
@@ -150,6 +161,32 @@ int hmmbw_comm_payload(const hmmbw_ctx *ctx, int64_t *n_doubles);
 int hmmbw_iterate_begin(hmmbw_ctx *ctx, int64_t n_seq_global, double **buf, int64_t *n_doubles);
 int hmmbw_iterate_end(hmmbw_ctx *ctx);
 
+/* ---- Peer all-reduce (HMMBW_OPT_ALLREDUCE = HMMBW_ALLREDUCE_PEER) ----
+ * The sums the reference forms over all recordings (pi over the global R, hmm_training.py:415-424; A and B,
+ * :429-500; L over all sequences, :503) are one elementwise sum of every rank's statistics buffer per EM
+ * iteration.  Instead of an RCCL all-reduce, every rank owns a RECEIVE REGION in its HBM with one slot per
+ * rank (double-buffered by iteration parity) and one flag per (rank, 2 KB chunk): after its E-step a rank
+ * writes its buffer into slot `rank` of every rank's region (system-scope write-through stores over xGMI,
+ * then the chunk's flag = the iteration's sequence number), and before its M-step it waits for all the
+ * flags of its own region (bounded: HMMBW_OPT_PEER_TIMEOUT_MS) and sums the slots in rank order, so every
+ * rank holds bitwise-identical sums and takes the same stop decision (:346).  Set-up, collective over the
+ * ranks (all call it, after hmmbw_set_rank and the options, before the first iteration):
+ *   hmmbw_peer_region     allocate this rank's receive region (*bytes; *region its device address);
+ *   hmmbw_peer_ipc_handle its 64-byte HIP IPC handle, to be exchanged between the rank processes;
+ *   hmmbw_peer_open       map every other rank's region from the exchanged handles (world x 64 bytes, in
+ *                         rank order) and attach them, or
+ *   hmmbw_peer_attach     attach regions already addressable here (world device pointers, rank order;
+ *                         several ranks in one process on one GPU, as the tests run it).
+ * n_seq_global is the R of hmm_training.py:424 over all ranks (hmmbw_iterate's loop).  Attaching clears
+ * the flags: every rank must attach before any rank starts an iteration. */
+int hmmbw_peer_region(hmmbw_ctx *ctx, void **region, int64_t *bytes);
+int hmmbw_peer_ipc_handle(hmmbw_ctx *ctx, void *handle_out);
+int hmmbw_peer_open(hmmbw_ctx *ctx, const void *handles, int64_t n_seq_global);
+int hmmbw_peer_attach(hmmbw_ctx *ctx, void *const *regions, int64_t n_seq_global);
+/* The all-reduce hmmbw_iterate and hmmbw_iterate_begin/_end use now: -1 none (single rank), 0 RCCL
+ * (engine communicator, or the caller's collective for _begin/_end), 1 peer. */
+int hmmbw_allreduce_kind(const hmmbw_ctx *ctx, int *kind);
+
 /* SYNC. Status plus the iteration records [first, first+count) (ring of 4096 entries). */
 int hmmbw_get_status(hmmbw_ctx *ctx, hmmbw_status *status, hmmbw_iter_record *records, int64_t first,
                      int64_t count);
@@ -201,6 +238,15 @@ int hmmbw_score(hmmbw_ctx *ctx, double *out);
  * other statistics' atomics.  Small state counts need the LDS emission tables (HMMBW_E_UNSUPPORTED
  * otherwise); set it before hmmbw_set_observations (HMMBW_E_STATE after).  Default 0. */
 #define HMMBW_OPT_DETERMINISTIC 7
+/* Multi-rank all-reduce of the per-iteration statistics: 0 (default) = RCCL (hmmbw_comm_init) or the
+ * caller's collective between hmmbw_iterate_begin and _end; 1 = the engine's own peer all-reduce
+ * (hmmbw_peer_* below; then _begin/_end do the whole exchange and the caller adds nothing between). */
+#define HMMBW_OPT_ALLREDUCE 8
+#define HMMBW_ALLREDUCE_RCCL 0
+#define HMMBW_ALLREDUCE_PEER 1
+/* Bound, in milliseconds, of the peer all-reduce's device-side wait for the other ranks' statistics
+ * (default 30000).  Past it the iteration fails with HMMBW_E_TIMEOUT instead of spinning. */
+#define HMMBW_OPT_PEER_TIMEOUT_MS 9
 int hmmbw_set_option(hmmbw_ctx *ctx, int key, int64_t value);
 
 /* E-step kernel timing with HIP events on the context stream (for bench/roofline).  Returns the
@@ -208,6 +254,11 @@ int hmmbw_set_option(hmmbw_ctx *ctx, int key, int64_t value);
  * mode: 0 off, k >= 1 record events around every k-th E-step launch (sampling keeps the event
  * overhead out of the timed loop); enable < 0 only queries. */
 int hmmbw_timing(hmmbw_ctx *ctx, int enable, double *total_ms, int64_t *count);
+/* The timed launches that run a follow-up kernel after the E-step kernel (the wide path's B-numerator
+ * gather, hmm_training.py:474-485; deterministic mode's fixed-order reductions): the accumulated time of
+ * the E-step kernel alone and the count (same reset as hmmbw_timing).  bench.py prices the fp64-MFMA
+ * bound on it. */
+int hmmbw_timing_split(hmmbw_ctx *ctx, double *estep_ms, int64_t *count);
 
 /* Vector-quantisation encoder: get_observations, hmm_training.py:82-120.  For every frame f, the index
  * of the nearest centroid (first minimum, strict '<' as at :111) by the Euclidean distance over the

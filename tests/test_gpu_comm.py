@@ -58,8 +58,9 @@ def test_native_comm_one_rank_matches_oracle(oracle, topology, maxit, N, K, eps,
         ranks, ar_ms, ar_n = e.comm_info()
         assert ranks == 1 and ar_n >= st.iterations and ar_ms > 0  # chunks past convergence still all-reduce
         copy_len = N + N * N + 2 * N + K * N
-        if not det:  # fused (small and wide): the copies + one (max, sum exp) pair per rank, 256-B aligned
-            nc = copies or 2
+        if not det:  # fused (small and wide): the copies + one (max, sum exp) pair per rank, 256-B aligned;
+            # the wide path all-reduces ONE copy (its B numerator is written once, by the gather)
+            nc = 1 if N > 16 else (copies or 2)
             assert e.comm_payload_bytes() == 8 * (-(-(nc * copy_len + 2) // 32) * 32)
         else:
             assert e.comm_payload_bytes() == 8 * e.stats_len

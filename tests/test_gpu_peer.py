@@ -1,0 +1,312 @@
+"""The engine's own peer all-reduce (HMMBW_OPT_ALLREDUCE = 1, include/hmmbw.h hmmbw_peer_*): after its E-step
+every rank writes its statistics buffer into slot `rank` of every rank's receive region and raises a flag per
+chunk; before its M-step it waits (bounded) for all the flags of its own region and sums the slots in rank
+order.  The sums it replaces are the reference's over all recordings: pi over the global R
+(hmm_training.py:415-424), A and B (:429-500) and L over all sequences (:503).
+
+On one GPU:
+* several ranks in ONE process (their regions attached by device pointer), each on its shard, through the
+  split-iteration ABI (all begins = E-step + push, then all ends = wait + sum + M-step, so no rank waits on a
+  push that is queued behind it), against the reference's fixtures and the oracle;
+* one rank through the native hmmbw_iterate loop (push to itself, wait, sum);
+* the bounded wait: a rank whose peer never pushes stops with HMMBW_E_TIMEOUT instead of spinning;
+* two PROCESSES on the same GPU, IPC handles exchanged over a gloo process group (the path an 8-GPU run
+  takes, minus xGMI), each rank ending on the oracle's parameters.
+"""
+import ctypes
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, ROOT
+
+pytestmark = pytest.mark.gpu
+
+PARAM_RTOL, PARAM_ATOL, LL_RTOL = 1e-6, 1e-15, 1e-9
+
+
+@pytest.fixture(scope="module", autouse=True)
+def gpu():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.fail("no HIP device visible: the GPU tests need an MI355X")
+
+
+def load(case):
+    return np.load(f"{GOLDEN}/bw_{case}.npz", allow_pickle=False)
+
+
+def observations(d):
+    off, sym = d["offsets"], d["symbols"]
+    return [sym[off[i]:off[i + 1]] for i in range(len(off) - 1)]
+
+
+def assert_params(mine, ref, what):
+    err = np.abs(np.asarray(mine) - ref) - (PARAM_RTOL * np.abs(ref) + PARAM_ATOL)
+    assert np.all(err <= 0), f"{what}: worst excess {err.max():.3e}"
+
+
+def attach_in_process(engines, timeout_ms=None):
+    """Peer regions of ranks living in this process, attached by device pointer (hmmbw_peer_attach); the
+    global R is the sum of the engines' shards."""
+    from hmm_training_amd._lib import ALLREDUCE, OPT_ALLREDUCE, OPT_PEER_TIMEOUT_MS, check
+    regions = []
+    for e in engines:
+        ptr, nb = ctypes.c_void_p(), ctypes.c_int64()
+        check(e._lib.hmmbw_peer_region(e._ctx, ctypes.byref(ptr), ctypes.byref(nb)))
+        assert nb.value > 0
+        regions.append(ptr.value)
+    arr = (ctypes.c_void_p * len(regions))(*regions)
+    R = sum(e.n_seq for e in engines)
+    for e in engines:
+        check(e._lib.hmmbw_peer_attach(e._ctx, arr, R))
+        check(e._lib.hmmbw_set_option(e._ctx, OPT_ALLREDUCE, ALLREDUCE["peer"]))
+        if timeout_ms is not None:
+            check(e._lib.hmmbw_set_option(e._ctx, OPT_PEER_TIMEOUT_MS, int(timeout_ms)))
+        assert e.allreduce == "peer"
+
+
+def run_world_peer(d, world, deterministic=False, iters=None):
+    from hmm_training_amd.engine import BaumWelchEngine, shard_bounds
+    N, M = int(d["N"]), int(d["M"])
+    obs = observations(d)
+    bounds = shard_bounds([len(o) for o in obs], world)
+    iters = int(d["max_iterations"]) + 1 if iters is None else iters
+    engines = []
+    try:
+        for r, (lo, hi) in enumerate(bounds):
+            e = BaumWelchEngine(N, M, rank=r, world_size=world, deterministic=deterministic)
+            e.set_observations(obs[lo:hi], n_seq_global=len(obs))
+            e.set_params(d["init_pi"], d["init_A"], d["init_B"])
+            e.reset(float(d["epsilon"]), int(d["max_iterations"]))
+            engines.append(e)
+        attach_in_process(engines)
+        # iterations past the stop rule are device-side no-ops on every rank (the reference stops there)
+        for _ in range(iters):
+            bufs = [e.iterate_begin() for e in engines]  # E-step + push to every rank's slot
+            assert len({n for _, n in bufs}) == 1
+            for e in engines:
+                e.iterate_end()                          # wait for every rank's flags, sum in rank order
+        out = []
+        for e in engines:
+            st, recs = e.status(0, int(d["iterations"]))
+            out.append((st, recs, e.params(normalise=False), e.params(normalise=True)))
+        return bounds, out
+    finally:
+        for e in engines:
+            e.close()
+
+
+CASES = ["n8_k256_t200", "converge", "zero_prob_seq", "dense_n16", "n64_k1024_tiny", "n5_k256_cfg1"]
+
+
+@pytest.mark.parametrize("deterministic", [False, True])
+@pytest.mark.parametrize("world", [2, 3, 8])
+@pytest.mark.parametrize("case", CASES)
+def test_peer_allreduce_in_process_matches_reference(case, world, deterministic):
+    d = load(case)
+    bounds, out = run_world_peer(d, world, deterministic)
+    for r, (st, recs, raw, (pi, A, B)) in enumerate(out):
+        assert st.done and st.iterations == int(d["iterations"]), f"rank {r} ({bounds[r]})"
+        np.testing.assert_allclose([x for x, _ in recs], d["trace_L"], rtol=LL_RTOL)
+        assert_params(A, d["out_A"], f"A rank {r}")
+        assert_params(B, d["out_B"], f"B rank {r}")
+        assert_params(pi, d["out_pi"], f"pi rank {r}")
+    # every rank sums the slots in rank order: bitwise-identical records and working parameters
+    st0, recs0, raw0, _ = out[0]
+    for r, (st, recs, raw, _) in enumerate(out[1:], 1):
+        assert recs == recs0, f"rank {r} L/diff records differ from rank 0"
+        for x, y in zip(raw, raw0):
+            np.testing.assert_array_equal(x, y)
+
+
+@pytest.mark.parametrize("N,K,topology,R,tmax,world", [(8, 256, "left_to_right", 2400, 160, 4),
+                                                        (8, 256, "dense", 2400, 160, 3),
+                                                        (40, 96, "dense", 700, 100, 5)])
+def test_peer_allreduce_vs_oracle(oracle_mt, N, K, topology, R, tmax, world):
+    """Hundreds of sequences per rank (several workgroups, the wide N = 40 path's tiles), 4 EM iterations,
+    against the oracle on the unsharded data: every log P, the L trace and (pi, A, B) on every rank."""
+    from hmm_training_amd.engine import BaumWelchEngine, shard_bounds, to_csr
+    from hmm_training_amd.hmm_training import default_initial_params
+    oracle = oracle_mt
+    rng = np.random.default_rng(31 * N + world)
+    iters = 4
+    obs = [rng.integers(0, K, size=int(t)) for t in rng.integers(20, tmax, size=R)]
+    pi, A, B = default_initial_params(N, K)
+    if topology == "dense":
+        A = 0.5 * A + 0.5 * rng.dirichlet(np.ones(N), size=N)
+    B = rng.dirichlet(np.full(K, 2.0), size=N)
+    off, sym = to_csr(obs)
+    ref = oracle.hmm_training(off, sym.astype(np.int64), N, K, 0.0, iters, pi, A, B)
+    bounds = shard_bounds([len(o) for o in obs], world)
+    engines = []
+    try:
+        for r, (lo, hi) in enumerate(bounds):
+            e = BaumWelchEngine(N, K, rank=r, world_size=world, topology=topology)
+            e.set_observations(obs[lo:hi], n_seq_global=R)
+            e.set_params(pi, A, B)
+            e.reset(0.0, iters)
+            engines.append(e)
+        attach_in_process(engines)
+        for _ in range(iters):
+            for e in engines:
+                e.iterate_begin()
+            for e in engines:
+                e.iterate_end()
+        res = [(e.status(0, iters), e.params(normalise=True), e.loglik()) for e in engines]
+    finally:
+        for e in engines:
+            e.close()
+    np.testing.assert_allclose(np.concatenate([r[2] for r in res]), ref.logP, rtol=LL_RTOL)
+    for r, ((st, recs), (p2, A2, B2), _) in enumerate(res):
+        assert st.iterations == iters and st.done
+        np.testing.assert_allclose([x for x, _ in recs], ref.trace_L, rtol=LL_RTOL)
+        assert recs == res[0][0][1]
+        assert_params(A2, ref.A, f"A rank {r}")
+        assert_params(B2, ref.B, f"B rank {r}")
+        assert_params(p2, ref.pi, f"pi rank {r}")
+
+
+@pytest.mark.parametrize("N,K,topology", [(8, 256, "left_to_right"), (40, 96, "dense")])
+def test_peer_native_loop_one_rank_matches_oracle(oracle, N, K, topology):
+    """hmmbw_iterate on a 1-rank context with the peer all-reduce attached to itself: the native loop
+    (E-step -> push -> wait + sum -> merged M-step) of an 8-GPU run, with the all-reduce timed."""
+    from hmm_training_amd._lib import check
+    from hmm_training_amd.engine import BaumWelchEngine
+    from hmm_training_amd.hmm_training import default_initial_params
+    rng = np.random.default_rng(23)
+    R, maxit = 500, 5
+    obs = [rng.integers(0, K, size=int(t)) for t in rng.integers(40, 220, size=R)]
+    pi, A, B = default_initial_params(N, K)
+    if topology == "dense":
+        A = 0.5 * A + 0.5 * rng.dirichlet(np.ones(N), size=N)
+    with BaumWelchEngine(N, K, device=0, topology=topology) as e:
+        check(e._lib.hmmbw_set_rank(e._ctx, 0, 1))
+        e.set_observations(obs)
+        e.set_params(pi, A, B)
+        attach_in_process([e])
+        e.timing(1)
+        trace = []
+        st = e.train(1e-6, maxit, lambda k, Lk, d: trace.append(Lk))
+        p2, A2, B2 = e.params()
+        _, ar_ms, ar_n = e.comm_info()
+        assert ar_n >= st.iterations and ar_ms > 0
+        assert e.comm_payload_bytes() > 0
+    off = np.concatenate([[0], np.cumsum([len(o) for o in obs])]).astype(np.int64)
+    ref = oracle.hmm_training(off, np.concatenate(obs).astype(np.int64), N, K, 1e-6, maxit, pi, A, B)
+    assert st.iterations == ref.iterations
+    np.testing.assert_allclose(trace, ref.trace_L, rtol=LL_RTOL)
+    for mine, theirs in ((A2, ref.A), (B2, ref.B), (p2, ref.pi)):
+        assert np.all(np.abs(mine - theirs) <= PARAM_RTOL * np.abs(theirs) + PARAM_ATOL)
+
+
+def test_peer_wait_is_bounded():
+    """Rank 1 never pushes: rank 0's wait ends after HMMBW_OPT_PEER_TIMEOUT_MS and EM stops with
+    HMMBW_E_TIMEOUT (an error from the status calls), not a spin."""
+    import time
+
+    from hmm_training_amd._lib import HMMBW_E_TIMEOUT, HMMBWError
+    from hmm_training_amd.engine import BaumWelchEngine
+    d = load("n8_k256_t200")
+    obs = observations(d)
+    N, M = int(d["N"]), int(d["M"])
+    engines = []
+    try:
+        for r in range(2):
+            e = BaumWelchEngine(N, M, rank=r, world_size=2)
+            e.set_observations(obs[r::2], n_seq_global=len(obs))
+            e.set_params(d["init_pi"], d["init_A"], d["init_B"])
+            e.reset(1e-6, 5)
+            engines.append(e)
+        attach_in_process(engines, timeout_ms=200)
+        e0 = engines[0]
+        t0 = time.perf_counter()
+        e0.iterate_begin()
+        e0.iterate_end()
+        with pytest.raises(HMMBWError) as ei:
+            e0.status()
+        assert ei.value.code == HMMBW_E_TIMEOUT
+        assert 0.15 < time.perf_counter() - t0 < 20.0
+        e0.iterate_begin()  # a stopped run's iterations are device-side no-ops (no second wait)
+        e0.iterate_end()
+        with pytest.raises(HMMBWError):
+            e0.status()
+    finally:
+        for e in engines:
+            e.close()
+
+
+WORKER = r"""
+import json, os, sys
+import numpy as np
+sys.path.insert(0, os.environ["HMMBW_ROOT"])
+import torch, torch.distributed as dist
+rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+dist.init_process_group("gloo")
+torch.cuda.set_device(0)
+from hmm_training_amd.engine import BaumWelchEngine, shard_bounds
+d = json.load(open(os.environ["HMMBW_CASE"]))
+obs = [np.asarray(o, dtype=np.int64) for o in d["obs"]]
+lo, hi = shard_bounds([len(o) for o in obs], world)[rank]
+with BaumWelchEngine(d["N"], d["K"], device=0, rank=rank, world_size=world, topology=d["topology"],
+                     allreduce="peer") as e:
+    e.set_observations(obs[lo:hi], n_seq_global=len(obs))
+    assert e.allreduce == "peer", e.allreduce
+    e.set_params(np.array(d["pi"]), np.array(d["A"]), np.array(d["B"]))
+    e.timing(1)
+    trace = []
+    st = e.train(0.0, d["iters"], lambda k, L, df: trace.append(L))
+    pi, A, B = e.params()
+    _, ar_ms, ar_n = e.comm_info()
+    json.dump({"trace": trace, "iterations": st.iterations, "pi": pi.tolist(), "A": A.tolist(), "B": B.tolist(),
+               "allreduce_us": 1e3 * ar_ms / max(ar_n, 1), "ar_n": ar_n},
+              open(os.environ["HMMBW_OUT"] + f".{rank}", "w"))
+dist.destroy_process_group()
+"""
+
+
+def test_peer_allreduce_two_processes_ipc(oracle_mt, tmp_path):
+    """Two rank processes on cuda:0: the IPC handles go through a gloo process group (all_gather_object),
+    each rank maps the other's region with hipIpcOpenMemHandle, and the engine's train() runs the native
+    peer loop.  Both ranks must end on the oracle's L trace and parameters."""
+    from hmm_training_amd.hmm_training import default_initial_params
+    rng = np.random.default_rng(41)
+    N, K, R, iters = 8, 256, 600, 4
+    obs = [rng.integers(0, K, size=int(t)) for t in rng.integers(40, 200, size=R)]
+    pi, A, B = default_initial_params(N, K)
+    case = {"N": N, "K": K, "topology": "left_to_right", "iters": iters, "obs": [o.tolist() for o in obs],
+            "pi": pi.tolist(), "A": A.tolist(), "B": B.tolist()}
+    cpath, opath = tmp_path / "case.json", tmp_path / "out"
+    cpath.write_text(json.dumps(case))
+    wpath = tmp_path / "worker.py"
+    wpath.write_text(WORKER)
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE="2", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                   HMMBW_ROOT=ROOT, HMMBW_CASE=str(cpath), HMMBW_OUT=str(opath))
+        procs.append(subprocess.Popen([sys.executable, str(wpath)], env=env))
+    try:
+        rcs = [p.wait(timeout=240) for p in procs]
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    assert rcs == [0, 0], rcs
+    off = np.concatenate([[0], np.cumsum([len(o) for o in obs])]).astype(np.int64)
+    ref = oracle_mt.hmm_training(off, np.concatenate(obs).astype(np.int64), N, K, 0.0, iters, pi, A, B)
+    outs = [json.load(open(f"{opath}.{r}")) for r in range(2)]
+    for r, o in enumerate(outs):
+        assert o["iterations"] == iters and o["ar_n"] >= iters
+        np.testing.assert_allclose(o["trace"], ref.trace_L, rtol=LL_RTOL)
+        assert_params(o["A"], ref.A, f"A rank {r}")
+        assert_params(o["B"], ref.B, f"B rank {r}")
+        assert_params(o["pi"], ref.pi, f"pi rank {r}")
+    assert outs[0]["trace"] == outs[1]["trace"]
