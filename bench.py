@@ -179,6 +179,7 @@ def find_traffic(cfg_key):
 
 SIMDS = 1024       # 256 CUs x 4 SIMDs (MI355X_MICROARCH.md chip-level parameters)
 VALU_CYCLES = 4    # wave64 fp64 VALU issue: 16 lanes per clock per SIMD (78.6 TF fp64 vector peak)
+VALU_CYCLES_32 = 2  # wave64 32-bit VALU issue on a SIMD-32 (MI355X_MICROARCH.md; a lone wave: 4)
 CLOCK_MAX_GHZ = 2.4  # MI355X max shader clock: the issue bound at the peak clock is the optimistic one
 MFMA_F64_CYCLES = 64  # v_mfma_f64_16x16x4_f64: 2,048 flops per SIMD every 64 cycles (78.6 TF / 1,024 SIMDs / 2.4 GHz)
 MFMA_F64_FLOPS = 2 * 16 * 16 * 4
@@ -198,6 +199,9 @@ def find_issue(cfg_key):
                 # GRBM_GUI_ACTIVE / 8 / kernel time reads high on dispatches under ~0.3 ms
                 # (MI355X_MICROARCH.md, DVFS give-back), so the bound is priced at the max clock
                 best = {"valu_insts_per_launch": float(k["SQ_INSTS_VALU"]), "clock_ghz": CLOCK_MAX_GHZ,
+                        "valu_fp64_per_launch": k.get("valu_fp64_insts"),
+                        "mfma_busy_cycles": k.get("SQ_VALU_MFMA_BUSY_CYCLES"),
+                        "lds_array_cycles": k.get("SQ_LDS_IDX_ACTIVE"),
                         "clock_ghz_grbm_estimate": k.get("clock_ghz"), "source": os.path.relpath(path, ROOT)}
     return best
 
@@ -219,11 +223,14 @@ def roofline_bounds(R, T, N, kern_s, traffic, issue, estep_s=None):
     frac is <= 1 when the measurement and the model are right; the binding bound is the largest frac.
 
     hbm        measured HBM bytes per launch (calibrated PMC FETCH/WRITE, profiles/) / kernel time vs 8 TB/s.
-    valu       all VALU instructions of the launch (SQ_INSTS_VALU) spread evenly over the 1,024 SIMDs,
-               4 cycles each (wave64 over 16 lanes) at the 2.4 GHz max clock.
-    simd_valu  the busiest SIMD's VALU pipe: by pigeonhole some SIMD runs ceil(waves / 1,024) waves, and it
-               must issue all their VALU instructions one after another (a SIMD's single VALU pipe), so
-               achieved = its issue rate over the kernel, peak = clock / 4.
+    valu       all VALU instructions of the launch (SQ_INSTS_VALU) spread evenly over the 1,024 SIMDs at the
+               2.4 GHz max clock: on a SIMD-32 a wave64 fp64 add / mul / fma / transcendental takes 4 cycles
+               (half the fp32 rate), every other VALU instruction 2 (MI355X_MICROARCH.md, SIMD-32), with the
+               fp64 share from the SQ_INSTS_VALU_{ADD,MUL,FMA,TRANS}_F64 counters.
+    simd_valu  the busiest SIMD: by pigeonhole some SIMD runs w = ceil(waves / 1,024) waves and must issue
+               all their VALU instructions on its one VALU pipe, max(w x (4 n64 + 2 (n - n64)), 4 n) cycles
+               for n VALU instructions per wave of which n64 fp64 (a single wave issues at most every 4
+               cycles); achieved / peak = that time / the kernel time, written as an issue rate.
     mfma, simd_mfma  (wide path) the same for the fp64 matrix pipe: every wave issues 48 dependent-block
                v_mfma_f64_16x16x4 per step (forward 4NT, backward 4NT, xi 4NT at NT = 4), 64 cycles each.
     """
@@ -248,17 +255,30 @@ def roofline_bounds(R, T, N, kern_s, traffic, issue, estep_s=None):
                             "frac": ach_s / peak_simd, "mfma_per_wave": mfma_wave,
                             "t_bound_us": 1e6 * wmax * mfma_wave * MFMA_F64_CYCLES / t_clock,
                             "kernel": "k_estep_mfma", "kernel_ms": 1e3 * t_e}
-    if issue and kern_s > 0 and N <= 16:
-        per_wave = issue["valu_insts_per_launch"] / waves
-        peak = t_clock / VALU_CYCLES / 1e9  # G VALU instructions / s of one SIMD
-        ach_bal = issue["valu_insts_per_launch"] / SIMDS / kern_s / 1e9
-        out["valu"] = {"achieved": ach_bal, "peak": peak, "unit": "G VALU instr/s per SIMD (mean)",
-                       "frac": ach_bal / peak, "valu_per_launch": issue["valu_insts_per_launch"],
-                       "source": issue["source"]}
-        ach_s = wmax * per_wave / kern_s / 1e9
-        out["simd_valu"] = {"achieved": ach_s, "peak": peak, "unit": "G VALU instr/s (busiest SIMD)",
-                            "frac": ach_s / peak, "valu_per_wave": per_wave,
-                            "t_bound_us": 1e6 * wmax * per_wave * VALU_CYCLES / t_clock, "source": issue["source"]}
+    if issue and kern_s > 0 and N <= 16 and issue.get("valu_fp64_per_launch") is not None:
+        n_all = issue["valu_insts_per_launch"]
+        n64 = issue["valu_fp64_per_launch"]
+        cyc_all = VALU_CYCLES * n64 + VALU_CYCLES_32 * (n_all - n64)  # SIMD-cycles of the whole launch
+        t_bal = cyc_all / SIMDS / t_clock
+        out["valu"] = {"achieved": t_bal / kern_s, "peak": 1.0, "unit": "fraction of SIMD VALU issue cycles (mean)",
+                       "frac": t_bal / kern_s, "t_bound_us": 1e6 * t_bal, "valu_per_launch": n_all,
+                       "valu_fp64_per_launch": n64, "source": issue["source"]}
+        nw, n64w = n_all / waves, n64 / waves
+        cyc_simd = max(wmax * (VALU_CYCLES * n64w + VALU_CYCLES_32 * (nw - n64w)), VALU_CYCLES * nw)
+        t_simd = cyc_simd / t_clock
+        out["simd_valu"] = {"achieved": t_simd / kern_s, "peak": 1.0,
+                            "unit": "fraction of the busiest SIMD's VALU issue cycles", "frac": t_simd / kern_s,
+                            "t_bound_us": 1e6 * t_simd, "valu_per_wave": nw, "valu_fp64_per_wave": n64w,
+                            "source": issue["source"]}
+    if issue and kern_s > 0 and N <= 16 and issue.get("lds_array_cycles"):
+        # the busiest CU's LDS array (shared by its 4 SIMDs): by pigeonhole some CU runs ceil(waves / 256)
+        # waves; SQ_LDS_IDX_ACTIVE = every LDS-array cycle of the launch, bank-conflict cycles included
+        cus = SIMDS // 4
+        wcu = -(-waves // cus)
+        t_lds = wcu * issue["lds_array_cycles"] / waves / t_clock
+        out["cu_lds"] = {"achieved": t_lds / kern_s, "peak": 1.0, "unit": "fraction of the busiest CU's LDS-array cycles",
+                         "frac": t_lds / kern_s, "t_bound_us": 1e6 * t_lds, "waves_on_busiest_cu": wcu,
+                         "lds_cycles_per_wave": issue["lds_array_cycles"] / waves, "source": issue["source"]}
     cands = {k: v for k, v in out.items() if isinstance(v, dict) and "frac" in v}
     out["binding"] = max(cands, key=lambda k: cands[k]["frac"]) if cands else None
     return out
@@ -603,18 +623,38 @@ def main(argv=None):
 
 
 def synced_protocol(eng, stats, world, dist, R, iters=10, dropin_iters=20):
-    """median of `iters` EM iterations, each followed by the 8-byte convergence read-back
-    (hmmbw_get_status), plus the drop-in train loop (BaumWelchEngine.train: chunked status syncs)
-    over `dropin_iters` iterations, in ms per iteration."""
+    """median of `iters` EM iterations, each followed by the host's read-back of the
+    convergence record (hmm_training.py:503-514), plus the drop-in train loop (BaumWelchEngine.train:
+    chunked status syncs) over `dropin_iters` iterations, in ms per iteration.
+
+    merged (the headline synced figure): after each iteration's launch, hmmbw_status_post enqueues a status
+    snapshot into pinned host memory and the host waits for that snapshot only.  The M-step of iteration e
+    runs in the prologue of launch e + 1, so the record the host reads after launch e + 1 is iteration e's:
+    every iteration is one launch plus one snapshot and one host wait, with no extra M-step kernel.
+    flush (kept for comparison): hmmbw_get_status after each iteration, which first runs the pending
+    M-step as its own kernel and synchronises the stream."""
     import torch
+    eng.status()
+    base = eng.status()[0].iterations
     per = []
+    for k in range(iters):
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        eng.enqueue_iterations(1, stats)
+        first = max(base + k - 1, 0)  # the record of the iteration whose M-step this launch ran
+        tk = eng.post_status(first)
+        st, _ = eng.wait_status(tk, first)  # the snapshot's pinned record, no stream-wide sync
+        per.append(time.perf_counter() - t0)
+    torch.cuda.synchronize()
+    per_flush = []
     for _ in range(iters):
         if world > 1:
             dist.barrier()
         t0 = time.perf_counter()
         eng.enqueue_iterations(1, stats)
-        eng.status()  # D2H of the convergence record (synchronises the engine stream)
-        per.append(time.perf_counter() - t0)
+        eng.status()  # the pending M-step as its own kernel, then the D2H (synchronises the engine stream)
+        per_flush.append(time.perf_counter() - t0)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -629,6 +669,8 @@ def synced_protocol(eng, stats, world, dist, R, iters=10, dropin_iters=20):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         med, dt = float(t[0]), float(t[1])
     return {"median_ms_per_iter_with_d2h": 1000.0 * med, "utt_per_s_with_d2h": R * world / med,
+            "protocol": "merged: launch + status snapshot (hmmbw_status_post/_wait) per iteration",
+            "median_ms_per_iter_with_flush": 1000.0 * float(np.median(per_flush)),
             "dropin_train_ms_per_iter": 1000.0 * dt / max(st.iterations, 1), "dropin_iterations": st.iterations}
 
 

@@ -138,25 +138,30 @@ __global__ void k_finalise(const double *pi, const double *A, const double *B, i
 // (hmm_training.py:415-424 pi over the global R, :429-500 A and B, :503 L) become ONE elementwise sum of
 // the ranks' statistics buffers per EM iteration.  Every rank owns a receive region in its HBM:
 //   [2 iteration parities][world slots][slot doubles], then flags [world][chunks] (uint64 sequence numbers)
-// k_peer_push  (after the E-step): workgroup (chunk c, peer p) writes chunk c of this rank's buffer into
-//              slot `rank` of p's region with system-scope write-through stores, waits for them
-//              (vmcnt(0) in every wave, then the barrier) and release-stores the iteration's sequence
-//              number into p's flag (rank, c);
-// k_peer_reduce (before the M-step): workgroup c's first wave polls its region's W flags of chunk c
-//              (system-scope loads + s_sleep, bounded by wall-clock ticks: on expiry the iteration
-//              state records HMMBW_E_TIMEOUT and stops EM), then sums the W slots in rank order into
-//              the buffer, so every rank holds bitwise-identical sums.
+// The buffer is cut into chunks of kPeerThreads x dpt doubles (dpt chosen so a payload has <= 32 chunks).
+//   push   workgroup (chunk c, peer p) writes chunk c of this rank's buffer into slot `rank` of p's region
+//          with system-scope write-through stores, waits for them (vmcnt(0) in every wave, then the
+//          barrier) and release-stores the iteration's sequence number into p's flag (rank, c);
+//   reduce workgroup c's first wave polls its region's W flags of chunk c (system-scope loads + s_sleep,
+//          bounded by wall-clock ticks: on expiry the iteration state records HMMBW_E_TIMEOUT and stops
+//          EM), then the workgroup sums the W slots in rank order into the buffer, so every rank holds
+//          bitwise-identical sums.
+// k_peer_allreduce does both in ONE launch (hmmbw_iterate's loop: one kernel boundary, as RCCL's);
+// the split ABI runs them as k_peer_push (in _begin) and k_peer_reduce (in _end), so several ranks that
+// share one stream (the in-process tests) never wait on a push queued behind them.
 // Parity double-buffering is enough: a rank can push iteration e + 2 into p's slot only after its own
 // reduce of e + 1, which needs p's push of e + 1, which p enqueues after its reduce of e.
 // ---------------------------------------------------------------------------------------------
 constexpr int kMaxPeers = 16;
-constexpr int kPeerChunk = 256;  // doubles per chunk = threads per workgroup
+constexpr int kPeerThreads = 256;
+constexpr int kPeerMaxChunks = 32;
 
 struct PeerArgs {
     double *region[kMaxPeers];  // every rank's receive region, as addressable from this device
     long long n;                // payload doubles
     long long slot;             // slot stride (n rounded up to 256 B)
-    long long nch;              // chunks of kPeerChunk doubles
+    long long nch;              // chunks
+    int dpt;                    // doubles per thread per chunk (chunk = kPeerThreads x dpt)
     int world, rank;
 };
 
@@ -164,14 +169,14 @@ __device__ __forceinline__ unsigned long long *peer_flags(double *region, const 
     return reinterpret_cast<unsigned long long *>(region + 2LL * P.world * P.slot);
 }
 
-__global__ void __launch_bounds__(kPeerChunk) k_peer_push(const double *src, PeerArgs P, unsigned long long seq,
-                                                          const IterState *state) {
-    if (state->done) return;  // identical on every rank: no rank pushes, none waits
-    const long long c = blockIdx.x;
-    const int p = blockIdx.y;
-    const long long i = c * kPeerChunk + threadIdx.x;
+__device__ __forceinline__ void peer_push_chunk(const double *src, const PeerArgs &P, unsigned long long seq,
+                                                long long c, int p) {
+    const long long base = c * kPeerThreads * P.dpt + threadIdx.x;
     double *dst = P.region[p] + ((long long)(seq & 1) * P.world + P.rank) * P.slot;
-    if (i < P.n) __hip_atomic_store(dst + i, src[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    for (int k = 0; k < P.dpt; ++k) {
+        const long long i = base + (long long)k * kPeerThreads;
+        if (i < P.n) __hip_atomic_store(dst + i, src[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's write-through stores are acknowledged
     __syncthreads();
     if (threadIdx.x == 0)
@@ -179,11 +184,10 @@ __global__ void __launch_bounds__(kPeerChunk) k_peer_push(const double *src, Pee
                            __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-__global__ void __launch_bounds__(kPeerChunk) k_peer_reduce(double *dst, PeerArgs P, unsigned long long seq,
-                                                            IterState *state, long long timeout_ticks) {
+// returns false (and stops EM with HMMBW_E_TIMEOUT) when a flag did not arrive in time
+__device__ __forceinline__ bool peer_reduce_chunk(double *dst, const PeerArgs &P, unsigned long long seq,
+                                                  IterState *state, long long timeout_ticks, long long c) {
     __shared__ int ok;
-    if (state->done) return;
-    const long long c = blockIdx.x;
     const int tid = threadIdx.x;
     double *reg = P.region[P.rank];
     if (tid < 64) {  // one wave polls: lane q watches rank q's flag of this chunk
@@ -205,17 +209,47 @@ __global__ void __launch_bounds__(kPeerChunk) k_peer_reduce(double *dst, PeerArg
             state->error = HMMBW_E_TIMEOUT;
             state->done = 1;
         }
-        return;
+        return false;
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: nothing stale from this device's caches
-    const long long i = c * kPeerChunk + tid;
-    if (i < P.n) {
-        const double *base = reg + (long long)(seq & 1) * P.world * P.slot + i;
-        double v = 0.0;
-        for (int q = 0; q < P.world; ++q)
-            v += __hip_atomic_load(base + q * P.slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        dst[i] = v;
+    const double *slots = reg + (long long)(seq & 1) * P.world * P.slot;
+    const long long base = c * kPeerThreads * P.dpt + tid;
+    for (int k = 0; k < P.dpt; ++k) {
+        const long long i = base + (long long)k * kPeerThreads;
+        if (i < P.n) {
+            double v = 0.0;
+            for (int q = 0; q < P.world; ++q)
+                v += __hip_atomic_load(slots + q * P.slot + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            dst[i] = v;
+        }
     }
+    return true;
+}
+
+__global__ void __launch_bounds__(kPeerThreads) k_peer_push(const double *src, PeerArgs P, unsigned long long seq,
+                                                            const IterState *state) {
+    if (state->done) return;  // identical on every rank: no rank pushes, none waits
+    peer_push_chunk(src, P, seq, blockIdx.x, blockIdx.y);
+}
+
+__global__ void __launch_bounds__(kPeerThreads) k_peer_reduce(double *dst, PeerArgs P, unsigned long long seq,
+                                                              IterState *state, long long timeout_ticks) {
+    if (state->done) return;
+    (void)peer_reduce_chunk(dst, P, seq, state, timeout_ticks, blockIdx.x);
+}
+
+// push + wait + sum in one launch: workgroup (c, p) pushes chunk c to rank p; the one whose p is this
+// rank (its own slot, the nearest memory) then waits for chunk c's W flags and sums them into `sum` (not
+// into buf, which the other workgroups of this launch may still be pushing).  At most 32 x 16 workgroups
+// of 256 threads, all resident at once, so a waiting workgroup never holds a slot a pushing one needs
+// (and every wait is bounded anyway).
+__global__ void __launch_bounds__(kPeerThreads) k_peer_allreduce(const double *buf, double *sum, PeerArgs P,
+                                                                 unsigned long long seq, IterState *state,
+                                                                 long long timeout_ticks) {
+    if (state->done) return;
+    peer_push_chunk(buf, P, seq, blockIdx.x, blockIdx.y);
+    if ((int)blockIdx.y != P.rank) return;
+    (void)peer_reduce_chunk(sum, P, seq, state, timeout_ticks, blockIdx.x);
 }
 
 __global__ void k_init_state(IterState *st, double eps, long long max_it) {
@@ -429,6 +463,7 @@ struct hmmbw_ctx {
     long long nblocks = 0;
     long long nfull = 0;          // small kernels: workgroups with 4 active waves (then xact-wave ones)
     int xact = 4;
+    int prio = 0;                 // diagnostics: HMMBW_PRIO at set_observations (see EArgs::prio)
     uint16_t *d_sym = nullptr;
     long long *d_wsym = nullptr, *d_wckoff = nullptr, *d_wspoff = nullptr;
     int *d_wT = nullptr, *d_wfull = nullptr, *d_slen = nullptr, *d_sseq = nullptr;
@@ -461,6 +496,8 @@ struct hmmbw_ctx {
     double *d_peer = nullptr;
     size_t peer_bytes = 0;
     long long peer_n = 0, peer_slot = 0, peer_nch = 0;
+    int peer_dpt = 1;
+    double *d_xsum = nullptr;     // the all-reduced sums the pending M-step reads (peer mode)
     int peer_world = 0;
     bool peer_on = false;
     std::vector<double *> peer_regions;
@@ -591,6 +628,7 @@ EArgs make_eargs(hmmbw_ctx *c) {
     a.off_bnum = c->off_bnum();
     a.nfull = c->nfull;
     a.xact = c->xact;
+    a.prio = c->prio;
     return a;
 }
 
@@ -992,6 +1030,7 @@ int hmmbw_ctx_destroy(hmmbw_ctx *c) {
     peer_detach(c);
     if (c->d_peer) (void)hipFree(c->d_peer);  // its own allocation (IPC-exported), not the block cache
     c->d_peer = nullptr;
+    dfree(c->d_xsum);
     free_obs(c);
     for (auto e : c->ev_free) (void)hipEventDestroy(e);
     for (auto e : c->ev_pending) (void)hipEventDestroy(e);
@@ -1232,6 +1271,7 @@ int hmmbw_set_observations(hmmbw_ctx *c, const int64_t *offsets, const int32_t *
     c->nblocks = nblocks;
     c->nfull = nfull;
     c->xact = xact;
+    if (const char *pe = std::getenv("HMMBW_PRIO")) c->prio = std::atoi(pe);
     c->has_obs = true;
     return ensure_zf(c);
 }
@@ -1433,6 +1473,7 @@ static PeerArgs peer_args(const hmmbw_ctx *c) {
     P.n = c->peer_n;
     P.slot = c->peer_slot;
     P.nch = c->peer_nch;
+    P.dpt = c->peer_dpt;
     P.world = c->peer_world;
     P.rank = c->rank;
     return P;
@@ -1443,17 +1484,33 @@ static int peer_push(hmmbw_ctx *c, const double *buf, long long len) {
         return fail(HMMBW_E_STATE, "the all-reduce payload changed after hmmbw_peer_region (rank, world or options "
                                    "set after it): set up the peer regions again");
     c->peer_seq += 1;
-    hipLaunchKernelGGL(k_peer_push, dim3((unsigned)c->peer_nch, (unsigned)c->peer_world), dim3(kPeerChunk), 0,
+    hipLaunchKernelGGL(k_peer_push, dim3((unsigned)c->peer_nch, (unsigned)c->peer_world), dim3(kPeerThreads), 0,
                        c->stream, buf, peer_args(c), c->peer_seq, c->state());
     HIP_TRY(hipGetLastError());
     return HMMBW_OK;
 }
 
-static int peer_reduce(hmmbw_ctx *c, double *buf) {
+// hmmbw_iterate's loop: push, wait and sum in one launch (k_peer_allreduce)
+static int peer_allreduce(hmmbw_ctx *c, double *buf, long long len) {
+    if (len != c->peer_n || c->peer_world != c->world)
+        return fail(HMMBW_E_STATE, "the all-reduce payload changed after hmmbw_peer_region (rank, world or options "
+                                   "set after it): set up the peer regions again");
+    c->peer_seq += 1;
     const long long ticks = std::max(1LL, c->peer_timeout_ms) * c->wall_khz;
-    hipLaunchKernelGGL(k_peer_reduce, dim3((unsigned)c->peer_nch), dim3(kPeerChunk), 0, c->stream, buf, peer_args(c),
-                       c->peer_seq, c->state(), ticks);
+    hipLaunchKernelGGL(k_peer_allreduce, dim3((unsigned)c->peer_nch, (unsigned)c->peer_world), dim3(kPeerThreads), 0,
+                       c->stream, buf, c->d_xsum, peer_args(c), c->peer_seq, c->state(), ticks);
     HIP_TRY(hipGetLastError());
+    c->ar_cur = c->d_xsum;  // the pending M-step reads the sums
+    return HMMBW_OK;
+}
+
+// the sums go to d_xsum, which becomes the pending M-step's source (mr_end)
+static int peer_reduce(hmmbw_ctx *c) {
+    const long long ticks = std::max(1LL, c->peer_timeout_ms) * c->wall_khz;
+    hipLaunchKernelGGL(k_peer_reduce, dim3((unsigned)c->peer_nch), dim3(kPeerThreads), 0, c->stream, c->d_xsum,
+                       peer_args(c), c->peer_seq, c->state(), ticks);
+    HIP_TRY(hipGetLastError());
+    c->ar_cur = c->d_xsum;
     return HMMBW_OK;
 }
 
@@ -1496,7 +1553,7 @@ int hmmbw_iterate_begin(hmmbw_ctx *c, int64_t n_seq_global, double **buf, int64_
 int hmmbw_iterate_end(hmmbw_ctx *c) {
     if (int rc = check_ready(c, true)) return rc;
     if (c->ar_open && c->peer_mode())
-        if (int rc = peer_reduce(c, c->ar_cur)) {
+        if (int rc = peer_reduce(c)) {
             c->ar_open = false;
             return rc;
         }
@@ -1509,7 +1566,9 @@ int hmmbw_peer_region(hmmbw_ctx *c, void **region, int64_t *bytes) {
     if (c->world > kMaxPeers) return fail(HMMBW_E_UNSUPPORTED, "peer all-reduce: at most 16 ranks");
     if (int rc = set_device(c)) return rc;
     const long long n = c->ar_payload();
-    const long long slot = (n + 31) / 32 * 32, nch = (n + kPeerChunk - 1) / kPeerChunk;
+    const long long dpt = std::min(64LL, std::max(1LL, (n + (long long)kPeerThreads * kPeerMaxChunks - 1) /
+                                                       ((long long)kPeerThreads * kPeerMaxChunks)));
+    const long long slot = (n + 31) / 32 * 32, nch = (n + kPeerThreads * dpt - 1) / (kPeerThreads * dpt);
     const size_t b = sizeof(double) * 2 * (size_t)c->world * (size_t)slot +
                      sizeof(unsigned long long) * (size_t)c->world * (size_t)nch;
     if (!c->d_peer || c->peer_n != n || c->peer_world != c->world) {
@@ -1520,10 +1579,14 @@ int hmmbw_peer_region(hmmbw_ctx *c, void **region, int64_t *bytes) {
         // its own allocation (exported with hipIpcGetMemHandle), never a block of the cache
         HIP_TRY(hipMalloc(reinterpret_cast<void **>(&c->d_peer), b));
         HIP_TRY(hipMemset(c->d_peer, 0, b));
+        dfree(c->d_xsum);
+        if (int rc = dalloc(&c->d_xsum, (size_t)slot)) return rc;
+        HIP_TRY(hipMemset(c->d_xsum, 0, sizeof(double) * (size_t)slot));
         c->peer_bytes = b;
         c->peer_n = n;
         c->peer_slot = slot;
         c->peer_nch = nch;
+        c->peer_dpt = (int)dpt;
         c->peer_world = c->world;
     }
     *region = c->d_peer;
@@ -1638,8 +1701,7 @@ int hmmbw_iterate(hmmbw_ctx *c, int64_t n_iter) {
                 // communicator tests then exercise the same ncclAllReduce call as an 8-GPU run
                 c->ar_len_last = ar_len;
                 if (peer) {
-                    if (int rc = peer_push(c, ar, ar_len)) return rc;
-                    if (int rc = peer_reduce(c, ar)) return rc;
+                    if (int rc = peer_allreduce(c, ar, ar_len)) return rc;
                 } else {
                     ncclResult_t e = r->all_reduce(ar, ar, (size_t)ar_len, ncclFloat64, ncclSum, c->comm, c->stream);
                     if (e != ncclSuccess) return rccl_fail(r, e, "ncclAllReduce");

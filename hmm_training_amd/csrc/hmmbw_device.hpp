@@ -151,6 +151,7 @@ struct EArgs {
     // the workgroups after them only xact (the waves beyond one per SIMD spread over more CUs)
     long long nfull;
     int xact;
+    int prio;          // diagnostics (HMMBW_PRIO): 1 = s_setprio 1 for the full workgroups' waves, 2 = for the extra ones
 };
 
 // Grouped launch (k_estep_small_group): per-model arguments and first workgroups (start[nm] = grid)
@@ -471,6 +472,8 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
 
     const int wpb = blockDim.x >> 6;
     const bool xblk = bid >= a.nfull;
+    if (a.prio == 1 && !xblk) __builtin_amdgcn_s_setprio(1);
+    if (a.prio == 2 && xblk) __builtin_amdgcn_s_setprio(1);
     const long long wave = xblk ? a.nfull * wpb + (bid - a.nfull) * a.xact + wv : bid * wpb + wv;
     const bool wactive = !xblk || wv < a.xact;
     double *accb = a.copies + (bid % a.ncopies) * a.copy_len;

@@ -389,6 +389,17 @@ class BaumWelchEngine:
                 mfh.close()
         return st
 
+    def post_status(self, first: int = 0) -> int:
+        """Enqueue a status snapshot (hmmbw_status_post: no M-step flush, the records of every iteration
+        enqueued so far but the last, whose M-step is merged into the next launch) and return its ticket."""
+        tk = ctypes.c_int64()
+        check(self._lib.hmmbw_status_post(self._ctx, int(first), ctypes.byref(tk)))
+        return tk.value
+
+    def wait_status(self, ticket: int, first: int = 0) -> Tuple[Status, List[Tuple[float, float]]]:
+        """Wait for snapshot `ticket` only (not for the work queued after it): status + records [first, ...)."""
+        return self._wait_status(ticket, first)
+
     def _wait_status(self, ticket: int, first: int) -> Tuple[Status, List[Tuple[float, float]]]:
         """Status snapshot `ticket` (hmmbw_status_wait) with the records of iterations [first, ...)."""
         st = Status()

@@ -47,6 +47,9 @@ def load():
         lib.oracle_lse.argtypes = [_dp, ctypes.c_int64]
         lib.oracle_set_threads.restype = ctypes.c_int
         lib.oracle_set_threads.argtypes = [ctypes.c_int]
+        lib.oracle_mstep_log.restype = None
+        lib.oracle_mstep_log.argtypes = [ctypes.c_int64, ctypes.c_int, ctypes.c_int, _dp, _dp, _dp, _dp, _dp, _dp,
+                                         _dp, _dp]
         _lib = lib
     return _lib
 
@@ -111,6 +114,30 @@ def estep_logstats(offsets, symbols, N, M, pi, A, B) -> OracleResult:
         raise RuntimeError(f"oracle_estep_logstats failed ({rc})")
     return OracleResult(log_pi_num=lpi_num, log_xi=lxi, log_gden_excl=lgex, log_gden_all=lgall, log_bnum=lbnum,
                         logP=logP[:R])
+
+
+def merge_logstats(parts) -> OracleResult:
+    """E-step statistics of a set of sequences from those of a partition of it (each an estep_logstats
+    result): every statistic is a log-sum over sequences (hmm_training.py:415-497), so the parts combine by
+    log-sum-exp (-inf parts drop out, as in the reference's log_sum_exp, :66-79); logP concatenated."""
+    def lse_all(name):
+        with np.errstate(invalid="ignore"):
+            return np.logaddexp.reduce(np.stack([getattr(p, name) for p in parts]), axis=0)
+    return OracleResult(log_pi_num=lse_all("log_pi_num"), log_xi=lse_all("log_xi"),
+                        log_gden_excl=lse_all("log_gden_excl"), log_gden_all=lse_all("log_gden_all"),
+                        log_bnum=lse_all("log_bnum"), logP=np.concatenate([p.logP for p in parts]))
+
+
+def mstep_log(R, N, M, s: OracleResult):
+    """The reference's M-step (hmm_training.py:415-500) from log statistics: (log_pi, log_A, log_B),
+    unnormalised, R counting every sequence (:424)."""
+    lpi, la, lb = np.zeros(N), np.zeros(N * N), np.zeros(N * M)
+    load().oracle_mstep_log(int(R), N, M, np.ascontiguousarray(s.log_pi_num, np.float64),
+                            np.ascontiguousarray(s.log_xi, np.float64).reshape(-1),
+                            np.ascontiguousarray(s.log_gden_excl, np.float64),
+                            np.ascontiguousarray(s.log_gden_all, np.float64),
+                            np.ascontiguousarray(s.log_bnum, np.float64).reshape(-1), lpi, la, lb)
+    return lpi, la.reshape(N, N), lb.reshape(N, M)
 
 
 def forward_loglik(offsets, symbols, N, M, pi, A, B) -> np.ndarray:

@@ -70,7 +70,7 @@ def test_bench_single_gpu_line():
     rf = d["roofline"]
     # the binding ceiling of the launch: every bound is achieved / peak of one resource, so frac <= 1;
     # the survey's byte model stays beside it (effective_bw_frac, not a bound: it can exceed 1)
-    assert rf["bound"] == rf["bounds"]["binding"] in ("hbm", "valu", "simd_valu")
+    assert rf["bound"] == rf["bounds"]["binding"] in ("hbm", "valu", "simd_valu", "cu_lds")
     assert 0 < rf["frac"] <= 1.0 and rf["frac"] == max(b["frac"] for b in rf["bounds"].values() if isinstance(b, dict))
     assert rf["effective_bw_frac"] > 0 and rf["bounds"]["waves_on_busiest_simd"] >= 1
     assert d["cpu_baseline"]["value"] > 0

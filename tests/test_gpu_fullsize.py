@@ -155,8 +155,8 @@ def test_cfg4_shard_full_size_vs_oracle(oracle_mt):
 
 
 def test_cfg4_whole_on_one_gpu_vs_oracle(oracle_mt):
-    """BASELINE cfg4 unsharded: 100,000 x T=200, N=8, K=256 on one GPU, one EM iteration + statistics."""
-    run_vs_oracle(oracle_mt, 100_000, 200, 8, 256, "left_to_right", 1, seed=44)
+    """BASELINE cfg4 unsharded: 100,000 x T=200, N=8, K=256 on one GPU, two EM iterations + statistics."""
+    run_vs_oracle(oracle_mt, 100_000, 200, 8, 256, "left_to_right", 2, seed=44)
 
 
 def test_cfg5_full_shape_slice_vs_oracle(oracle_mt):
@@ -182,42 +182,127 @@ def test_cfg5_slice_deterministic_vs_oracle(oracle_mt):
     run_vs_oracle(oracle_mt, 1024, 400, 64, 1024, "dense", 2, seed=56, deterministic=True)
 
 
-def test_cfg5_whole_on_one_gpu(oracle_mt):
-    """BASELINE cfg5 unsharded: 50,000 x T=400, N=64, K=1024, dense on ONE GPU (20 GB of alpha_hat and
-    gamma rows; the reference's per-utterance xi allocation, hmm_training.py:328-339, cannot run it), 2 EM
-    iterations: the L trace against the per-sequence log P, sum rules, the M-step against the reference
-    formulas, and 64 sampled sequences' log P against oracle.forward_loglik (hmm_testing.py:49-104)."""
-    from hmm_training_amd.engine import BaumWelchEngine, StatsLayout
-    oracle = oracle_mt
-    R, T, N, K = 50_000, 400, 64, 1024
-    sym = _symbols(R, T, N, K, "U", 5)
-    off = np.arange(R + 1, dtype=np.int64) * T
-    pi, A, B = _params(N, K, "dense", 5)
-    with BaumWelchEngine(N, K, topology="dense") as eng:
-        eng.set_observations(offsets=off, symbols=sym)
-        eng.set_params(pi, A, B)
-        eng.reset(0.0, 2)
-        eng.enqueue_iterations(2)
-        st, recs = eng.status(0, 2)
-        assert st.iterations == 2
-        lp = eng.loglik()
-        assert np.all(np.isfinite(lp))
-        assert np.isclose(recs[-1][0], oracle.lse(lp), rtol=1e-12)
-        p_cur, A_cur, B_cur = eng.params(normalise=False)
-        g, ll, (p_m, A_m, B_m) = statistics_pass(eng, N, K, R)
-    np.testing.assert_allclose(g["B_num"].sum(1), g["gamma_den_all"], rtol=1e-11)
-    np.testing.assert_allclose(g["xi"].sum(1), g["gamma_den_excl"], rtol=1e-11)
-    assert np.isclose(g["pi_num"].sum(), R, rtol=1e-12)
-    assert np.isclose(g["gamma_den_all"].sum(), R * T, rtol=1e-12)
-    hp, hA, hB = host_mstep(g, R)
-    np.testing.assert_allclose(p_m, hp, rtol=1e-12, atol=1e-300)
-    np.testing.assert_allclose(A_m, hA, rtol=1e-12, atol=1e-300)
-    np.testing.assert_allclose(B_m, hB, rtol=1e-12, atol=1e-300)
-    pick = np.sort(np.random.default_rng(6).choice(R, size=64, replace=False))
-    ref = oracle.forward_loglik(np.arange(len(pick) + 1) * T, sym.reshape(R, T)[pick].reshape(-1).astype(np.int64),
-                                N, K, p_cur, A_cur, B_cur)
-    np.testing.assert_allclose(ll[pick], ref, rtol=LL_RTOL)
-    assert np.isclose(StatsLayout.lse_of_pairs(g["ll_pairs"]), oracle.lse(ll), rtol=1e-12)
+CFG5_WHOLE = dict(R=50_000, T=400, N=64, K=1024, world=4, seed=5)
+_cfg5_oracle_parts = {}
+
+
+@pytest.fixture(scope="module")
+def cfg5_whole_gpu():
+    """BASELINE cfg5 unsharded: 50,000 x T=400, N=64, K=1024, dense, ONE EM iteration on ONE GPU as four
+    ranks of 12,500 sequences (the reference's per-utterance xi allocation, hmm_training.py:328-339, cannot
+    run it at all), through the split-iteration ABI, which runs the kernels of a 4-GPU job: each rank's
+    partial statistics (the buffer it would all-reduce) and log P are kept for the per-quarter oracle
+    comparisons, then the buffers are summed and every rank applies the M-step (:415-514)."""
+    import torch
+    from hmm_training_amd.engine import BaumWelchEngine, StatsLayout, shard_bounds
+    c = CFG5_WHOLE
+    R, T, N, K, W = c["R"], c["T"], c["N"], c["K"], c["world"]
+    sym = _symbols(R, T, N, K, "U", c["seed"])
+    pi, A, B = _params(N, K, "dense", c["seed"])
+    bounds = shard_bounds([T] * R, W)
+    layout = StatsLayout(N, K, W)
+    engines, parts = [], []
+    try:
+        for r, (lo, hi) in enumerate(bounds):
+            e = BaumWelchEngine(N, K, rank=r, world_size=W, topology="dense")
+            e.set_observations(offsets=np.arange(hi - lo + 1, dtype=np.int64) * T, symbols=sym[lo * T:hi * T],
+                               n_seq_global=R)
+            e.set_params(pi, A, B)
+            e.reset(0.0, 1)
+            engines.append(e)
+        bufs = [e.iterate_begin() for e in engines]
+        torch.cuda.synchronize()
+        tot = None
+        for (ptr, n), e in zip(bufs, engines):
+            x = torch.empty(n, dtype=torch.float64, device="cuda:0")
+            torch.cuda.synchronize()
+            hip_copy(x.data_ptr(), ptr, 8 * n)
+            parts.append(layout.decode(x[:layout.length].cpu().numpy()))
+            tot = x.clone() if tot is None else tot + x
+        for ptr, n in bufs:
+            hip_copy(ptr, tot.data_ptr(), 8 * n)
+        logp = [e.loglik() for e in engines]
+        for e in engines:
+            e.iterate_end()
+        res = []
+        for e in engines:
+            st, recs = e.status(0, 1)
+            res.append((st, recs, e.params(normalise=False), e.params(normalise=True)))
+    finally:
+        for e in engines:
+            e.close()
+    return dict(sym=sym, params=(pi, A, B), bounds=bounds, parts=parts, logp=logp, res=res, layout=layout)
+
+
+def hip_copy(dst, src, nbytes):
+    import os
+
+    import torch
+    h = ctypes.CDLL(os.path.join(os.path.dirname(torch.__file__), "lib", "libamdhip64.so"))
+    h.hipMemcpy.restype = ctypes.c_int
+    h.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    torch.cuda.synchronize()
+    assert h.hipMemcpy(ctypes.c_void_p(dst), ctypes.c_void_p(src), nbytes, 3) == 0
+    torch.cuda.synchronize()
+
+
+def _cfg5_oracle_part(oracle, run, q):
+    if q not in _cfg5_oracle_parts:
+        c = CFG5_WHOLE
+        lo, hi = run["bounds"][q]
+        T, N, K = c["T"], c["N"], c["K"]
+        pi, A, B = run["params"]
+        _cfg5_oracle_parts[q] = oracle.estep_logstats(np.arange(hi - lo + 1, dtype=np.int64) * T,
+                                                      run["sym"][lo * T:hi * T].astype(np.int64), N, K, pi, A, B)
+    return _cfg5_oracle_parts[q]
+
+
+@pytest.mark.parametrize("q", [0, 1, 2, 3])
+def test_cfg5_whole_quarter_statistics_vs_oracle(oracle_mt, cfg5_whole_gpu, q):
+    """One quarter (12,500 sequences) of the whole cfg5 set: that rank's COMPLETE partial statistics
+    (pi_num, xi, gamma_den_excl, gamma_den_all, B_num: hmm_training.py:388-497) at rtol 1e-9, every log P
+    (:375-377) at rtol 1e-9 and the rank's (max, sum exp) pair against the oracle on the same sequences."""
+    from hmm_training_amd.engine import StatsLayout
+    run = cfg5_whole_gpu
+    c = CFG5_WHOLE
+    lo, hi = run["bounds"][q]
+    s = _cfg5_oracle_part(oracle_mt, run, q)
+    g = run["parts"][q]
+    np.testing.assert_allclose(run["logp"][q], s.logP, rtol=LL_RTOL)
+    with np.errstate(under="ignore"):
+        for key, lkey in (("pi_num", "log_pi_num"), ("xi", "log_xi"), ("gamma_den_excl", "log_gden_excl"),
+                          ("gamma_den_all", "log_gden_all"), ("B_num", "log_bnum")):
+            np.testing.assert_allclose(g[key], np.exp(getattr(s, lkey)), rtol=STAT_RTOL, atol=1e-300, err_msg=key)
+    assert np.isclose(g["pi_num"].sum(), hi - lo, rtol=1e-12)
+    assert np.isclose(g["gamma_den_all"].sum(), (hi - lo) * c["T"], rtol=1e-12)
+    pair = g["ll_pairs"][q]
+    assert np.all(np.delete(g["ll_pairs"], q, axis=0) == 0.0)  # only this rank's slot is written
+    assert np.isclose(StatsLayout.lse_of_pairs(pair), oracle_mt.lse(s.logP), rtol=1e-12)
+
+
+def test_cfg5_whole_iteration_vs_oracle(oracle_mt, cfg5_whole_gpu):
+    """The whole cfg5 set's EM iteration: the oracle's statistics of the four quarters merged (log-sum-exp,
+    hmm_training.py:66-79) and its M-step (:415-500), against every rank's parameters after the
+    all-reduce (working and returned, :524-541), and L (:503) over all 50,000 log P."""
+    run = cfg5_whole_gpu
+    c = CFG5_WHOLE
+    R, N, K = c["R"], c["N"], c["K"]
+    s = oracle_mt.merge_logstats([_cfg5_oracle_part(oracle_mt, run, q) for q in range(c["world"])])
+    lpi, la, lb = oracle_mt.mstep_log(R, N, K, s)
+    L = oracle_mt.lse(s.logP)
+    with np.errstate(under="ignore"):
+        epi, eA, eB = np.exp(lpi), np.exp(la), np.exp(lb)
+    for r, (st, recs, (p_cur, A_cur, B_cur), (p_out, A_out, B_out)) in enumerate(run["res"]):
+        assert st.iterations == 1 and st.done
+        assert np.isclose(recs[0][0], L, rtol=LL_RTOL), f"rank {r}"
+        assert_params(p_cur, epi, f"log_pi rank {r}")
+        assert_params(A_cur, eA, f"log_A rank {r}")
+        assert_params(B_cur, eB, f"log_B rank {r}")
+        assert_params(p_out, epi / epi.sum(), f"pi rank {r}")
+        assert_params(A_out, eA / eA.sum(1, keepdims=True), f"A rank {r}")
+        assert_params(B_out, eB / eB.sum(1, keepdims=True), f"B rank {r}")
+        for x, y in zip((p_cur, A_cur, B_cur), run["res"][0][2]):
+            np.testing.assert_array_equal(x, y)  # replicated: bitwise-identical on every rank
 
 
 @pytest.mark.parametrize("xact,topology", [(None, "left_to_right"), ("1", "left_to_right"), ("3", "left_to_right"),

@@ -132,3 +132,29 @@ def test_oracle_threads_match_serial(oracle):
     np.testing.assert_allclose(many.trace_L, one.trace_L, rtol=1e-13)
     for a, b in ((many.A, one.A), (many.B, one.B), (many.pi, one.pi)):
         np.testing.assert_allclose(a, b, rtol=1e-11, atol=1e-300)
+
+
+def test_oracle_merge_and_mstep_helpers(oracle):
+    """merge_logstats of a partition equals the statistics of the whole set, and mstep_log applied to them
+    equals the M-step inside oracle.hmm_training (hmm_training.py:415-500): the helpers the whole-cfg5
+    parity test combines its per-quarter oracle runs with."""
+    from hmm_training_amd.hmm_training import default_initial_params
+    rng = np.random.default_rng(12)
+    N, K, T, R = 5, 16, 30, 40
+    pi, A, B = default_initial_params(N, K)
+    off = np.arange(R + 1, dtype=np.int64) * T
+    sym = rng.integers(0, K, size=R * T).astype(np.int64)
+    full = oracle.estep_logstats(off, sym, N, K, pi, A, B)
+    parts = [oracle.estep_logstats(off[:14] - off[0], sym[:13 * T], N, K, pi, A, B),
+             oracle.estep_logstats(off[:28] - off[0], sym[13 * T:40 * T], N, K, pi, A, B)]
+    m = oracle.merge_logstats(parts)
+    for k in ("log_pi_num", "log_xi", "log_gden_excl", "log_gden_all", "log_bnum"):
+        x, y = getattr(m, k), getattr(full, k)
+        assert np.array_equal(np.isfinite(x), np.isfinite(y)), k
+        np.testing.assert_allclose(x[np.isfinite(y)], y[np.isfinite(y)], rtol=0, atol=1e-12, err_msg=k)
+    np.testing.assert_array_equal(m.logP, full.logP)
+    lpi, la, lb = oracle.mstep_log(R, N, K, full)
+    ref = oracle.hmm_training(off, sym, N, K, 0.0, 1, pi, A, B)
+    np.testing.assert_array_equal(lpi, ref.log_pi)
+    np.testing.assert_array_equal(la, ref.log_A)
+    np.testing.assert_array_equal(lb, ref.log_B)

@@ -14,14 +14,14 @@ declare -A KER=([lr_cfg3]=k_estep_small [lrH_cfg3]=k_estep_small [dense_cfg3]=k_
                 [cfg5]="k_estep_mfma,k_bnum_gather" [cfg4shard]=k_estep_small)
 for W in lr_cfg3 lrH_cfg3 dense_cfg3 cfg5 cfg4shard; do
   cp "$SRC/trace_$W/run_kernel_stats.csv" "profiles/$DEST/kernel_stats_$W.csv"
-  for C in FETCH_SIZE WRITE_SIZE SQ; do
+  for C in FETCH_SIZE WRITE_SIZE SQ SQ2; do
     cp "$SRC/pmc_${C}_$W/run_counter_collection.csv" "profiles/$DEST/pmc_${C}_$W.csv"
   done
   python3 tools/traffic_summary.py --fetch "profiles/$DEST/pmc_FETCH_SIZE_$W.csv" \
     --write "profiles/$DEST/pmc_WRITE_SIZE_$W.csv" \
     --calib-fetch "profiles/$DEST/pmc_calib_FETCH_SIZE.csv" --calib-write "profiles/$DEST/pmc_calib_WRITE_SIZE.csv" \
     --kernel "${KER[$W]}" --config-key "${KEY[$W]}" --out "profiles/$DEST/traffic_$W.json"
-  python3 tools/pmc_summary.py "profiles/$DEST/pmc_SQ_$W.csv" "${KER[$W]}" --config-key "${KEY[$W]}" \
+  python3 tools/pmc_summary.py "profiles/$DEST/pmc_SQ_$W.csv,profiles/$DEST/pmc_SQ2_$W.csv" "${KER[$W]}" --config-key "${KEY[$W]}" \
     --kernel-stats "profiles/$DEST/kernel_stats_$W.csv" > "profiles/$DEST/sq_$W.json"
 done
 for W in cfg2 vq; do

@@ -29,10 +29,11 @@ def main():
     ap.add_argument("--no-merge", action="store_true")
     ap.add_argument("--iters", type=int, default=6)
     ap.add_argument("--kwaves", type=int, default=0, help="kernel waves to read (default: R / sequences per wave)")
+    ap.add_argument("--lib", default=None, help="prebuilt diagnostics library (default hmm_training_amd/libhmmbw_phase.so)")
     a = ap.parse_args()
     out_dir = os.path.join(ROOT, "gpurun_out", "phase")
     os.makedirs(out_dir, exist_ok=True)
-    lib = os.path.join(ROOT, "hmm_training_amd", "libhmmbw_phase.so")  # prebuilt in-tree if present
+    lib = a.lib or os.path.join(ROOT, "hmm_training_amd", "libhmmbw_phase.so")  # prebuilt in-tree if present
     if not os.path.exists(lib):
         from hmm_training_amd import build as B
         B.build(force=True, defines=["-DHMMBW_PHASE_TIMES"], out=lib, tag="phase")

@@ -23,7 +23,9 @@ def mean_ns(stats_csv, kern):
 
 
 def main(src, kernels, config_key=None, kernel_stats=None):
-    files = [src] if os.path.isfile(src) else glob.glob(f"{src}/p*/run_counter_collection.csv")
+    files = []
+    for one in src.split(","):  # several CSVs (separate counter passes of the same workload) merge
+        files += [one] if os.path.isfile(one) else glob.glob(f"{one}/p*/run_counter_collection.csv")
     out = {}
     for kern in kernels.split(","):
         vals = collections.defaultdict(list)
@@ -38,6 +40,10 @@ def main(src, kernels, config_key=None, kernel_stats=None):
             for c in ("SQ_INSTS_VALU", "SQ_INSTS_LDS"):
                 if c in d:
                     d[c.lower() + "_per_wave"] = d[c] / d["SQ_WAVES"]
+        f64 = sum(d.get(c, 0.0) for c in ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64",
+                                          "SQ_INSTS_VALU_TRANS_F64"))
+        if "SQ_INSTS_VALU_FMA_F64" in d:
+            d["valu_fp64_insts"] = f64  # 4-cycle issue on a SIMD-32 (half the fp32 rate); the rest 2 cycles
         d["dispatches"] = max((len(v) for v in vals.values()), default=0)
         if config_key:
             d["config_key"] = config_key
