@@ -627,14 +627,33 @@ def synced_protocol(eng, stats, world, dist, R, iters=10, dropin_iters=20):
     convergence record (hmm_training.py:503-514), plus the drop-in train loop (BaumWelchEngine.train:
     chunked status syncs) over `dropin_iters` iterations, in ms per iteration.
 
-    merged (the headline synced figure): after each iteration's launch, hmmbw_status_post enqueues a status
-    snapshot into pinned host memory and the host waits for that snapshot only.  The M-step of iteration e
-    runs in the prologue of launch e + 1, so the record the host reads after launch e + 1 is iteration e's:
-    every iteration is one launch plus one snapshot and one host wait, with no extra M-step kernel.
+    The M-step of iteration e runs in the prologue of launch e + 1, so the record the host reads after
+    enqueueing launch e + 1 is iteration e's, and the host decides on it before enqueueing launch e + 2.
+    live (the headline synced figure, HMMBW_OPT_LIVE_STATUS): that prologue also writes the record into
+    pinned host memory, which the host polls (hmmbw_status_live_wait), so the read-back overlaps the rest of
+    launch e + 1.  snapshot: after each launch hmmbw_status_post enqueues a status snapshot kernel and the
+    host waits for that snapshot (the launch's end) before enqueueing again.
     flush (kept for comparison): hmmbw_get_status after each iteration, which first runs the pending
     M-step as its own kernel and synchronises the stream."""
     import torch
     eng.status()
+    base = eng.status()[0].iterations
+    # live (the headline): the M-step in launch e + 1's prologue writes iteration e's record into pinned
+    # host memory while that launch runs; the host polls it (hmmbw_status_live_wait) and enqueues the
+    # next launch as soon as it has read it, so the record of every iteration is read back before the
+    # iteration after next starts and the GPU never waits for the host
+    eng.live_status(True)
+    per_live = []
+    for k in range(iters + 1):
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        eng.enqueue_iterations(1, stats)
+        if k >= 1:
+            st, _ = eng.wait_live(base + k)  # iteration base + k - 1's record, from this launch's prologue
+            per_live.append(time.perf_counter() - t0)
+    torch.cuda.synchronize()
+    eng.live_status(False)
     base = eng.status()[0].iterations
     per = []
     for k in range(iters):
@@ -663,13 +682,17 @@ def synced_protocol(eng, stats, world, dist, R, iters=10, dropin_iters=20):
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     med = float(np.median(per))
+    med_live = float(np.median(per_live))
     if world > 1:
-        t = torch.tensor([med, dt], dtype=torch.float64,
+        t = torch.tensor([med, dt, med_live], dtype=torch.float64,
                          device=f"cuda:{eng.device}" if dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        med, dt = float(t[0]), float(t[1])
-    return {"median_ms_per_iter_with_d2h": 1000.0 * med, "utt_per_s_with_d2h": R * world / med,
-            "protocol": "merged: launch + status snapshot (hmmbw_status_post/_wait) per iteration",
+        med, dt, med_live = float(t[0]), float(t[1]), float(t[2])
+    return {"median_ms_per_iter_with_d2h": 1000.0 * med_live, "utt_per_s_with_d2h": R * world / med_live,
+            "protocol": "live: per iteration one launch, then the host polls the pinned convergence record that "
+                        "the next launch's merged M-step writes (hmmbw_status_live_wait) before enqueueing again",
+            "median_ms_per_iter_snapshot": 1000.0 * med,
+            "protocol_snapshot": "launch + status snapshot kernel (hmmbw_status_post/_wait) per iteration",
             "median_ms_per_iter_with_flush": 1000.0 * float(np.median(per_flush)),
             "dropin_train_ms_per_iter": 1000.0 * dt / max(st.iterations, 1), "dropin_iterations": st.iterations}
 

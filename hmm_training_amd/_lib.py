@@ -39,9 +39,9 @@ EXPORTED = (
     "hmmbw_group_timing", "hmmbw_vq_encode", "hmmbw_comm_unique_id", "hmmbw_comm_init",
     "hmmbw_comm_probe", "hmmbw_comm_info", "hmmbw_comm_payload", "hmmbw_iterate_begin", "hmmbw_iterate_end",
     "hmmbw_cache_trim", "hmmbw_timing_split", "hmmbw_peer_region", "hmmbw_peer_ipc_handle", "hmmbw_peer_open",
-    "hmmbw_peer_attach", "hmmbw_allreduce_kind",
+    "hmmbw_peer_attach", "hmmbw_allreduce_kind", "hmmbw_status_live_wait",
 )
-ABI_VERSION = 3
+ABI_VERSION = 4
 OPT_SAFE_SCALING = 1
 OPT_ABLATE = 2
 OPT_STAT_COPIES = 3
@@ -49,6 +49,7 @@ OPT_MERGE_MSTEP = 4
 OPT_DETERMINISTIC = 7
 OPT_ALLREDUCE = 8
 OPT_PEER_TIMEOUT_MS = 9
+OPT_LIVE_STATUS = 10
 ALLREDUCE = {"rccl": 0, "peer": 1}
 
 
@@ -98,6 +99,8 @@ def _declare(lib):
         "hmmbw_status_post": (ctypes.c_int, [c_ctx, ctypes.c_int64, P(ctypes.c_int64)]),
         "hmmbw_status_wait": (ctypes.c_int, [c_ctx, ctypes.c_int64, P(Status), ctypes.c_void_p, ctypes.c_int64,
                                              ctypes.c_int64]),
+        "hmmbw_status_live_wait": (ctypes.c_int, [c_ctx, ctypes.c_int64, P(Status), ctypes.c_void_p, ctypes.c_int64,
+                                                  ctypes.c_int64]),
         "hmmbw_get_params": (ctypes.c_int, [c_ctx, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
         "hmmbw_get_loglik": (ctypes.c_int, [c_ctx, ctypes.c_void_p]),
         "hmmbw_score": (ctypes.c_int, [c_ctx, ctypes.c_void_p]),

@@ -53,6 +53,15 @@ constexpr int kXs = 17;        // LDS row stride (doubles) of a [state][16 seque
 // state it captures by reference (beta, gamma sums) in scratch memory
 #define HMMBW_AI __attribute__((always_inline))
 
+// max over the 4 rows (16 lanes each) of a wave, for every in-row lane: one v_permlane16_swap (rows
+// 0<->1, 2<->3) and one v_permlane32_swap (halves); each returns the pair (own, partner)
+__device__ __forceinline__ int row_max4(int x) {
+    const auto r16 = __builtin_amdgcn_permlane16_swap((unsigned)x, (unsigned)x, false, false);
+    x = max((int)r16[0], (int)r16[1]);
+    const auto r32 = __builtin_amdgcn_permlane32_swap((unsigned)x, (unsigned)x, false, false);
+    return max((int)r32[0], (int)r32[1]);
+}
+
 __device__ __forceinline__ f64x4 mfma_f64(double a, double b, f64x4 c) {
     return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
 }
@@ -164,8 +173,17 @@ __global__ void __launch_bounds__(NT * 64, 2) k_estep_mfma(EArgs a) {  // 2 wave
             int M = 0;
 #pragma unroll
             for (int kb = 0; kb < KB; ++kb) M = max(M, bexp(zb[kb]));
-            M = max(M, __shfl_xor(M, 16));
-            M = max(M, __shfl_xor(M, 32));
+            // across the 4 lane rows: gfx950's row-swap permutes are VALU ops (ds_bpermute put two LDS
+            // round trips in front of the MFMA chain, which the compiler schedules after them)
+            M = row_max4(M);
+            // the exponent's VALU work between the chain's MFMAs (each waits ~64 cycles for the last)
+            // instead of in front of the first one
+            __builtin_amdgcn_sched_group_barrier(0x100, KB / 2, 0);
+#pragma unroll
+            for (int kb = 0; kb < KB; ++kb) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+            }
             sc = M == 0 ? 0 : M - 1023;
             // rescale before the emission factor: z_{t-1} and b(o_t) may both be ~1e-200 (no underflow)
 #pragma unroll
@@ -269,10 +287,12 @@ __global__ void __launch_bounds__(NT * 64, 2) k_estep_mfma(EArgs a) {  // 2 wave
         f64x4 S[NT];
 #pragma unroll
         for (int mm = 0; mm < NT; ++mm) S[mm] = f64x4{0.0, 0.0, 0.0, 0.0};
-        // rings: alpha_hat_t (HBM) in slot t % 2, loaded two steps ahead; b(o_{t+1}) (L2-resident
-        // table) and s_{t+1} in slot t % 2, loaded one step ahead (fewer VGPRs: two waves per SIMD)
+        // rings (two slots each, indexed by step parity: fewer VGPRs, two waves per SIMD): alpha_hat_t
+        // (HBM), loaded two visits before the publish that uses it; b(o_t) (L2-resident table) and s_t,
+        // loaded one visit before
         f64x4 zring[2], bring1[2];
         int sring[2];
+        f64x4 zs;  // z_t masked to the regular steps: gamma_t of the step that consumes the image
         auto ldz = [&](int t) HMMBW_AI -> f64x4 {
             f64x4 v;
             if (WIDE_ABL(a, 8)) return f64x4{0.5, 0.5, 0.5, 0.5};
@@ -280,15 +300,14 @@ __global__ void __launch_bounds__(NT * 64, 2) k_estep_mfma(EArgs a) {  // 2 wave
             for (int r = 0; r < 4; ++r) v[r] = ckw[((long long)t * NT * 4 + r) * 64];
             return v;
         };
-        // one regular step t <= Tw - 2 (MASK: per-sequence t <= T - 2 in ragged tiles)
-        auto bstep = [&](int t, const f64x4 &zt, const f64x4 &b1, int s1, auto MASK_, auto STEADY_) HMMBW_AI {
+        // publish(t): the image of step t <= Tw - 2 (MASK: per-sequence t <= T - 2 in ragged tiles) into
+        // LDS buffer t % 2: v_{t+1}(j) = b_j(o_{t+1}) 2^{-s_{t+1}} beta_hat_{t+1}(j) (:182-197) and z_t
+        auto publish = [&](int t, const f64x4 &zt, const f64x4 &b1, int s1, auto MASK_) HMMBW_AI {
             constexpr bool MASK = decltype(MASK_)::value;
-            constexpr bool STEADY = decltype(STEADY_)::value;
             const bool reg = !MASK || t <= T - 2;
-            f64x4 v, zs;
+            f64x4 v;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                // v_j = b_j(o_{t+1}) 2^{-s_{t+1}} beta_hat_{t+1}(j) (:182-197)
                 v[r] = __builtin_amdgcn_ldexp(b1[r] * beta[r], -s1);
                 if constexpr (MASK) {
                     v[r] = reg ? v[r] : 0.0;
@@ -297,23 +316,30 @@ __global__ void __launch_bounds__(NT * 64, 2) k_estep_mfma(EArgs a) {  // 2 wave
                     zs[r] = zt[r];
                 }
             }
+            put(putb, t & 1, v);
+            put(putb + 2 * IMG, t & 1, zs);
+        };
+        // consume(t): after the barrier, beta_hat_t = A v_{t+1} (:163-199, this wave's 16 rows), gamma_t,
+        // then the xi MFMAs of the same image.  The xi products are off the beta chain: they are made
+        // to follow it (a register dependency on beta_t), so that the next step's image is computed
+        // and published (VALU, LDS writes) between them instead of after them, and the wave reaches
+        // the next barrier right after its last MFMA issues.
+        auto consume = [&](int t, auto MASK_, auto STEADY_, auto &&next) HMMBW_AI {
+            constexpr bool MASK = decltype(MASK_)::value;
+            constexpr bool STEADY = decltype(STEADY_)::value;
+            const bool reg = !MASK || t <= T - 2;
             const int p = t & 1;
-            put(putb, p, v);
-            put(putb + 2 * IMG, p, zs);
             if (!WIDE_ABL(a, 16)) __syncthreads();
-            // beta_hat_t = A v (:163-199), this wave's 16 rows
             const double *vsrc = bopb + p * IMG;
             f64x4 acc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
             for (int kb = 0; kb < KB; ++kb) acc = mfma_f64(aop[kb], vsrc[4 * kb * kXs], acc);
             // S_ij += sum_s z_t(i, s) v_{t+1}(j, s): xi_t(i,j) / a_ij (:396-410)
             const double *tsrc = topb + p * IMG;
+            double za[4];
 #pragma unroll
-            for (int kk = 0; kk < 4; ++kk) {
-                const double za = tsrc[2 * IMG + 16 * m * kXs + 4 * kk];
-#pragma unroll
-                for (int mj = 0; mj < NT; ++mj) S[mj] = mfma_f64(za, tsrc[16 * mj * kXs + 4 * kk], S[mj]);
-            }
+            for (int kk = 0; kk < 4; ++kk) za[kk] = tsrc[2 * IMG + 16 * m * kXs + 4 * kk];
+            asm volatile("" : "+v"(za[0]) : "v"(acc[0]));  // xi after the beta chain (see above)
             f64x4 gm;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
@@ -323,6 +349,10 @@ __global__ void __launch_bounds__(NT * 64, 2) k_estep_mfma(EArgs a) {  // 2 wave
                 else beta[r] = bn;
                 gex[r] += gm[r];
             }
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+                for (int mj = 0; mj < NT; ++mj) S[mj] = mfma_f64(za[kk], tsrc[16 * mj * kXs + 4 * kk], S[mj]);
             if ((!MASK || reg) && !WIDE_ABL(a, 4)) putg(t, gm);  // B numerator row (:474-485)
             if (!STEADY && t == 0) {  // pi_num (:415-420): gamma_0 summed over the tile's sequences
 #pragma unroll
@@ -333,39 +363,44 @@ __global__ void __launch_bounds__(NT * 64, 2) k_estep_mfma(EArgs a) {  // 2 wave
                     else if (s == 0 && j < N && x != 0.0) unsafeAtomicAdd(&accb[j], x);
                 }
             }
+            next();  // publish(t - 1), when there is a step t - 1
         };
         uint4 pc;  // chunk c's symbol pack; chunk c - 1's is loaded at the top of chunk c
+        // visit t: consume(t) for t <= Tw - 2, publish(t - 1) for 1 <= t <= Tw - 1 (with b(o_t), s_t
+        // from slot t % 2), then b(o_{t-1}), s_{t-1} and alpha_hat_{t-3} into the slots just consumed
         auto bchunk = [&](int c, auto MASK_, auto STEADY_) HMMBW_AI {
             constexpr bool STEADY = decltype(STEADY_)::value;  // c >= 1 and every step t <= Tw - 2
             const uint4 pp = loadpack(c >= 1 ? c - 1 : 0);
 #pragma unroll
             for (int k = kChunk - 1; k >= 0; --k) {
                 const int t = c * kChunk + k;
-                // b(o_t), s_t and alpha_hat_{t - kLook} into the slots step t + 1 has consumed; the
-                // one-step-ahead loads go first so that waiting for them (in-order vmcnt) leaves
-                // the deeper alpha_hat prefetch in flight
-                if (STEADY || t >= 1) {
-                    bring1[(k + 1) & 1] = emis(sym_of(pc, k));  // b(o_t), consumed by step t - 1
-                    sring[(k + 1) & 1] = ew[t * kTileSeqs];     // s_t
-                }
+                auto pub = [&]() HMMBW_AI {
+                    if (STEADY || (t >= 1 && t <= Tw - 1))
+                        publish(t - 1, zring[(k + 1) & 1], bring1[k & 1], sring[k & 1], MASK_);
+                };
                 // tile-uniform; gamma_{T-1} is done above
-                if (STEADY || t <= Tw - 2) bstep(t, zring[k & 1], bring1[k & 1], sring[k & 1], MASK_, STEADY_);
-                // alpha_hat_{t-2} into the slot step t has just consumed (two in flight: VGPR budget)
-                if (STEADY || t >= 2) zring[k & 1] = ldz(t - 2);
+                if (STEADY || t <= Tw - 2) consume(t, MASK_, STEADY_, pub);
+                else pub();
+                if (STEADY || t >= 2) {
+                    bring1[(k + 1) & 1] = emis(k >= 1 ? sym_of(pc, k - 1) : sym_of(pp, kChunk - 1));  // b(o_{t-1})
+                    sring[(k + 1) & 1] = ew[(t - 1) * kTileSeqs];                                   // s_{t-1}
+                }
+                if (STEADY || t >= 3) zring[(k + 1) & 1] = ldz(t - 3);
             }
             pc = pp;
         };
         auto backward = [&](auto MASK_) HMMBW_AI {
             const int ttop = nch * kChunk;  // steps ttop - 1 .. 0 are visited (those > Tw - 2 skip)
             pc = loadpack(nch - 1);
-            // alpha_hat of the first two visited steps s = ttop - 1 - i; step ttop - 1 has no o_{s+1}
+            // alpha_hat for the first two visits' publish: z_{ttop-2}, z_{ttop-3}
 #pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                const int s0 = ttop - 1 - i;
+            for (int i = 2; i < 4; ++i) {
+                const int s0 = ttop - i;
                 zring[s0 & 1] = s0 >= 0 ? ldz(s0) : f64x4{0.0, 0.0, 0.0, 0.0};
             }
-            bring1[1] = f64x4{0.0, 0.0, 0.0, 0.0};
-            sring[1] = 0;
+            // b(o_{ttop-1}), s_{ttop-1} for the first visit (slot 1: ttop - 1 is odd)
+            bring1[1] = emis(sym_of(pc, kChunk - 1));
+            sring[1] = ew[(ttop - 1) * kTileSeqs];
             // chunks [1, cs] have every step t <= Tw - 2 (c * kChunk + kChunk - 1 <= Tw - 2)
             const int cs = Tw >= kChunk + 1 ? (Tw - kChunk - 1) / kChunk : 0;
             int c = nch - 1;

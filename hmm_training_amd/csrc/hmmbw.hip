@@ -32,6 +32,7 @@
 //   k_finalise  the reference's return-path normalisation (:524-541).
 #include <dlfcn.h>
 
+#include <atomic>
 #include <cstdlib>
 #include <map>
 #include <mutex>
@@ -179,8 +180,11 @@ __device__ __forceinline__ void peer_push_chunk(const double *src, const PeerArg
     }
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's write-through stores are acknowledged
     __syncthreads();
+    // The flag is a write-through store too, issued after every payload store of the workgroup was
+    // acknowledged: that orders it after them.  A release would add an L2 write-back at system scope
+    // (every dirty line of this XCD, e.g. the E-step's checkpoints), which the payload does not need.
     if (threadIdx.x == 0)
-        __hip_atomic_store(peer_flags(P.region[p], P) + (long long)P.rank * P.nch + c, seq, __ATOMIC_RELEASE,
+        __hip_atomic_store(peer_flags(P.region[p], P) + (long long)P.rank * P.nch + c, seq, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
@@ -211,7 +215,8 @@ __device__ __forceinline__ bool peer_reduce_chunk(double *dst, const PeerArgs &P
         }
         return false;
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: nothing stale from this device's caches
+    // no acquire fence (it would invalidate this XCD's L2): the slot loads below are system-scope loads,
+    // which bypass the caches and are issued after the flags were seen
     const double *slots = reg + (long long)(seq & 1) * P.world * P.slot;
     const long long base = c * kPeerThreads * P.dpt + tid;
     for (int k = 0; k < P.dpt; ++k) {
@@ -439,6 +444,9 @@ struct hmmbw_ctx {
         long long ticket = -1;
     } snaps[2];
     long long snap_next = 0;
+    // HMMBW_OPT_LIVE_STATUS: the host mirror every recording M-step writes (hmmbw_status_live_wait)
+    LiveBlock *h_live = nullptr;
+    unsigned live_epoch = 1;
     double *d_copies = nullptr;   // [3][ncopies][copy_len] E-step accumulators (iteration e uses e % 3)
     int ncopies = 2;              // HMMBW_OPT_STAT_COPIES default: halves the flush atomics per address (measured -3 %)
     bool merge_mstep = true;      // run each M-step in the prologue of the next E-step launch
@@ -659,6 +667,8 @@ MArgs make_margs(hmmbw_ctx *c, const hmmbw_ctx::Pending &p) {
     m.off_S = c->off_S();
     m.off_gex = c->off_gex();
     m.off_gall = c->off_gall();
+    m.live = c->h_live;
+    m.live_epoch = c->live_epoch;
     m.off_bnum = c->off_bnum();
     m.off_ll = c->off_ll();
     return m;
@@ -1022,6 +1032,7 @@ int hmmbw_ctx_destroy(hmmbw_ctx *c) {
         cached_free(sn.hist, kPinnedBlock);
     }
     dfree(c->d_state); dfree(c->d_hist); dfree(c->d_copies); dfree(c->d_ext); dfree(c->d_xbuf); dfree(c->d_ctr);
+    cached_free(c->h_live, kPinnedBlock);
     if (c->comm) {
         Rccl *r = nullptr;
         if (rccl_load(nullptr, &r) == HMMBW_OK) (void)r->comm_destroy(c->comm);
@@ -1315,6 +1326,26 @@ int hmmbw_set_option(hmmbw_ctx *c, int key, int64_t value) {
         c->peer_timeout_ms = value;
         return HMMBW_OK;
     }
+    if (key == HMMBW_OPT_LIVE_STATUS) {
+        if (int rc = set_device(c)) return rc;
+        HIP_TRY(hipStreamSynchronize(c->stream));  // no launch of the old setting is still in flight
+        if (value == 0) {
+            cached_free(c->h_live, kPinnedBlock);
+            c->h_live = nullptr;
+            return HMMBW_OK;
+        }
+        if (c->h_live) return HMMBW_OK;
+        HIP_TRY(cached_alloc(reinterpret_cast<void **>(&c->h_live), sizeof(LiveBlock), kPinnedBlock));
+        // seed the mirror with the state as it stands (records of a pending M-step follow when it runs)
+        IterState h{};
+        HIP_TRY(hipMemcpy(&h, c->state(), sizeof(IterState), hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(c->h_live->hist, c->d_hist, sizeof(double) * 2 * (size_t)kHist, hipMemcpyDeviceToHost));
+        c->h_live->slot[h.iteration & 1] = h;
+        std::atomic_thread_fence(std::memory_order_release);
+        reinterpret_cast<volatile unsigned long long &>(c->h_live->pub) =
+            ((unsigned long long)c->live_epoch << 32) | (unsigned long long)(unsigned)h.iteration;
+        return HMMBW_OK;
+    }
     if (key == HMMBW_OPT_ABLATE) {  // diagnostics: results are wrong while set
         c->ablate = (int)value;
         return HMMBW_OK;
@@ -1357,6 +1388,7 @@ int hmmbw_reset_training(hmmbw_ctx *c, double epsilon, int64_t max_iterations) {
     if (int rc = flush_mstep(c)) return rc;
     hipLaunchKernelGGL(k_init_state, dim3(1), dim3(1), 0, c->stream, c->state(), epsilon, (long long)max_iterations);
     HIP_TRY(hipGetLastError());
+    ++c->live_epoch;  // the mirror's records of the previous run no longer count (hmmbw_status_live_wait)
     HIP_TRY(hipMemsetAsync(c->d_copies, 0, sizeof(double) * 3 * c->ncopies * c->copy_len(), c->stream));
     if (c->d_xbuf) HIP_TRY(hipMemsetAsync(c->d_xbuf, 0, sizeof(double) * 3 * (size_t)c->xlen, c->stream));
     c->e_count = 0;
@@ -1827,6 +1859,69 @@ int hmmbw_status_wait(hmmbw_ctx *c, int64_t ticket, hmmbw_status *st, hmmbw_iter
             const int64_t k = first + i - sn.first;
             rec[i].log_likelihood = sn.hist[2 * k];
             rec[i].diff = sn.hist[2 * k + 1];
+        }
+    }
+    return HMMBW_OK;
+}
+
+int hmmbw_status_live_wait(hmmbw_ctx *c, int64_t iterations, hmmbw_status *st, hmmbw_iter_record *rec,
+                           int64_t first, int64_t count) {
+    if (!c || !st) return fail(HMMBW_E_INVALID, "null argument");
+    if (!c->h_live) return fail(HMMBW_E_STATE, "HMMBW_OPT_LIVE_STATUS is off");
+    if (int rc = set_device(c)) return rc;
+    volatile LiveBlock *lv = c->h_live;
+    IterState h{};
+    bool have = false;
+    for (long long spin = 0;; ++spin) {
+        const unsigned long long p0 = lv->pub;
+        std::atomic_thread_fence(std::memory_order_acquire);
+        if ((unsigned)(p0 >> 32) == c->live_epoch) {
+            const long long n = (long long)(unsigned)(p0 & 0xffffffffULL);
+            const volatile IterState &sl = lv->slot[n & 1];
+            h.prev_L = sl.prev_L;
+            h.last_L = sl.last_L;
+            h.last_diff = sl.last_diff;
+            h.epsilon = sl.epsilon;
+            h.iteration = sl.iteration;
+            h.max_iterations = sl.max_iterations;
+            h.done = sl.done;
+            h.converged = sl.converged;
+            h.error = sl.error;
+            std::atomic_thread_fence(std::memory_order_acquire);
+            const unsigned long long p1 = lv->pub;
+            // the slot is rewritten only by the record after next: two publications apart
+            const bool stable = (unsigned)(p1 >> 32) == c->live_epoch && (long long)(unsigned)(p1 & 0xffffffffULL) <= n + 1;
+            if (stable && h.iteration == n && (n >= iterations || h.done)) {
+                have = true;
+                break;
+            }
+        }
+        // the stream ran dry without the record (a pending M-step, a device-side stop the mirror does not
+        // carry, or a reset): the device state is the answer
+        if ((spin & 63) == 63 && hipStreamQuery(c->stream) == hipSuccess) {
+            const unsigned long long p2 = lv->pub;
+            if ((unsigned)(p2 >> 32) == c->live_epoch && (long long)(unsigned)(p2 & 0xffffffffULL) >= iterations) continue;
+            break;
+        }
+    }
+    std::vector<double> dh;
+    if (!have) {
+        HIP_TRY(hipMemcpy(&h, c->state(), sizeof(IterState), hipMemcpyDeviceToHost));
+        if (rec && count > 0) {
+            dh.resize(2 * (size_t)kHist);
+            HIP_TRY(hipMemcpy(dh.data(), c->d_hist, sizeof(double) * dh.size(), hipMemcpyDeviceToHost));
+        }
+    }
+    fill_status(h, st);
+    if (h.error) return fail(h.error, "EM stopped on a device-side failure: a rank did not deliver its statistics to "
+                                      "the peer all-reduce within HMMBW_OPT_PEER_TIMEOUT_MS");
+    if (rec && count > 0) {
+        if (first < 0 || first + count > h.iteration || first < h.iteration - kHist)
+            return fail(HMMBW_E_INVALID, "requested iteration records are not available");
+        for (int64_t i = 0; i < count; ++i) {
+            const int64_t k = (first + i) % kHist;
+            rec[i].log_likelihood = have ? lv->hist[2 * k] : dh[2 * k];
+            rec[i].diff = have ? lv->hist[2 * k + 1] : dh[2 * k + 1];
         }
     }
     return HMMBW_OK;

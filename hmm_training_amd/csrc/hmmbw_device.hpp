@@ -102,6 +102,17 @@ struct Layout {
     long long nwaves;
 };
 
+// Host-visible mirror of the convergence state (HMMBW_OPT_LIVE_STATUS), in fine-grained pinned host
+// memory: every M-step that records an iteration also writes the record and the new state here with
+// write-through stores, then publishes pub = epoch << 32 | iteration.  The state goes to slot
+// iteration % 2, so a reader that sees pub unchanged around its copy of that slot read one record.
+struct LiveBlock {
+    unsigned long long pub;
+    unsigned long long pad_[7];
+    IterState slot[2];
+    double hist[2 * kHist];  // (L, diff) of iteration i at 2 (i % kHist)
+};
+
 struct MArgs {
     const double *src;     // statistics: the copies (single rank) or the all-reduced buffer
     double *zero_ll;       // LL slots to clear (multi-rank) or nullptr
@@ -118,6 +129,8 @@ struct MArgs {
     int local_lse;
     int bt_perm;           // 1: B^T columns in the wide kernels' order (wide_col)
     long long off_S, off_gex, off_gall, off_bnum, off_ll;
+    LiveBlock *live;       // HMMBW_OPT_LIVE_STATUS: the host mirror (or nullptr)
+    unsigned live_epoch;   // the host's reset count: records of an earlier run never match
 };
 
 struct EArgs {
@@ -381,6 +394,16 @@ constexpr int kHistOff = kTabPad ? 40960 : 32768;
 __host__ __device__ constexpr bool lds_tables_fit(int K, int GP) { return (size_t)K * GP * 16 <= (size_t)kHistOff; }
 __host__ __device__ constexpr size_t lds_table_bytes(int K, int GP) { return (size_t)kHistOff + (size_t)K * GP * 16; }
 
+// Entry i = k * GP + c (symbol k, state column c) of the LDS emission tables, 16 B each:
+// P {a_cc b_c(k), a_{c-1,c} b_c(k)} (left-to-right, PT) or {b_c(k), 0} (dense); H {histogram, b_c(k)}.
+// (Round 4 measured a dense layout with two 8-B copies of b per row, one per sequence-slot parity, to
+// spread the ds_read_b64 lane groups over more banks: 74.0-76.7 us at cfg3 against 73.4, no gain.)
+template <bool PT, int GP>
+__device__ __forceinline__ void tab_put(double *sP, double *sH, int i, double px, double py, double b) {
+    reinterpret_cast<double2 *>(sP)[i] = PT ? double2{px, py} : double2{b, 0.0};
+    reinterpret_cast<double2 *>(sH)[i] = double2{0.0, b};
+}
+
 template <int N, int G, int GP, bool PT, int BLK = kBlock>
 __device__ bool merged_mstep(const EArgs &a, double *sP, double *sH, double *sPA, long long bid);
 __device__ int rank_ll_count(const EArgs &a);
@@ -457,11 +480,10 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
                             const int c = i % GP;
                             const double ad = c < N ? sPA[G + c * N + c] : 0.0;
                             const double ai = (c >= 1 && c < N) ? sPA[G + (c - 1) * N + c] : 0.0;
-                            reinterpret_cast<double2 *>(sP)[i] = double2{ad * x[q], ai * x[q]};
+                            tab_put<PT, GP>(sP, sH, i, ad * x[q], ai * x[q], x[q]);
                         } else {
-                            reinterpret_cast<double2 *>(sP)[i] = double2{x[q], 0.0};
+                            tab_put<PT, GP>(sP, sH, i, 0.0, 0.0, x[q]);
                         }
-                        reinterpret_cast<double2 *>(sH)[i] = double2{0.0, x[q]};
                     }
                 }
             }
@@ -1212,6 +1234,23 @@ __device__ bool record_iteration(const MArgs &m, const IterState &in, double L) 
         o.converged = (it + 1 < in.max_iterations) ? 1 : 0;
     }
     *m.state_out = o;
+    if (m.live != nullptr) {  // the host mirror: record and state first, then (acknowledged) the publication
+        auto sys = [](auto *p, auto v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); };
+        sys(&m.live->hist[2 * (it % kHist)], L);
+        sys(&m.live->hist[2 * (it % kHist) + 1], diff);
+        IterState *sl = &m.live->slot[o.iteration & 1];
+        sys(&sl->prev_L, o.prev_L);
+        sys(&sl->last_L, o.last_L);
+        sys(&sl->last_diff, o.last_diff);
+        sys(&sl->epsilon, o.epsilon);
+        sys(&sl->iteration, o.iteration);
+        sys(&sl->max_iterations, o.max_iterations);
+        sys(&sl->done, o.done);
+        sys(&sl->converged, o.converged);
+        sys(&sl->error, o.error);
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): every store above is acknowledged
+        sys(&m.live->pub, ((unsigned long long)m.live_epoch << 32) | (unsigned long long)(unsigned)o.iteration);
+    }
     return cont;
 }
 
@@ -1623,11 +1662,10 @@ __device__ bool merged_mstep(const EArgs &a, double *sP, double *sH, double *sPA
             if constexpr (PT) {
                 const double ad = kSameState ? ad0 : a_of(jj, jj);
                 const double ai = kSameState ? ai0 : (jj >= 1 ? a_of(jj - 1, jj) : 0.0);
-                reinterpret_cast<double2 *>(sP)[i] = double2{ad * bval[q], ai * bval[q]};
+                tab_put<PT, GP>(sP, sH, i, ad * bval[q], ai * bval[q], bval[q]);  // histogram zeroed, b
             } else {
-                reinterpret_cast<double2 *>(sP)[i] = double2{bval[q], 0.0};
+                tab_put<PT, GP>(sP, sH, i, 0.0, 0.0, bval[q]);
             }
-            reinterpret_cast<double2 *>(sH)[i] = double2{0.0, bval[q]};  // this launch's histogram, b
         }
     }
     if (w0) {
@@ -1646,8 +1684,7 @@ __device__ bool merged_mstep(const EArgs &a, double *sP, double *sH, double *sPA
     if constexpr (GP > N) {
         for (int i = tid; i < K * (GP - N); i += BLK) {
             const int k = i / (GP - N), c = N + (i - k * (GP - N));
-            reinterpret_cast<double2 *>(sP)[k * GP + c] = double2{0.0, 0.0};
-            reinterpret_cast<double2 *>(sH)[k * GP + c] = double2{0.0, 0.0};
+            tab_put<PT, GP>(sP, sH, k * GP + c, 0.0, 0.0, 0.0);
         }
     }
     __syncthreads();

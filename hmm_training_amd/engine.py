@@ -25,7 +25,8 @@ from typing import Callable, List, Optional, Sequence, Tuple
 import numpy as np
 import torch
 
-from ._lib import (ALLREDUCE, OPT_ALLREDUCE, OPT_DETERMINISTIC, OPT_MERGE_MSTEP, OPT_PEER_TIMEOUT_MS, OPT_SAFE_SCALING,
+from ._lib import (ALLREDUCE, OPT_ALLREDUCE, OPT_DETERMINISTIC, OPT_LIVE_STATUS, OPT_MERGE_MSTEP, OPT_PEER_TIMEOUT_MS,
+                   OPT_SAFE_SCALING,
                    OPT_STAT_COPIES, TOPOLOGY, TOPOLOGY_NAME, IterRecord, Status, check, lib)
 
 IterCallback = Callable[[int, float, float], None]
@@ -395,6 +396,22 @@ class BaumWelchEngine:
         tk = ctypes.c_int64()
         check(self._lib.hmmbw_status_post(self._ctx, int(first), ctypes.byref(tk)))
         return tk.value
+
+    def live_status(self, on: bool = True) -> None:
+        """HMMBW_OPT_LIVE_STATUS: the M-steps mirror every iteration record into pinned host memory, which
+        wait_live() polls (synchronises the engine stream once, when switched)."""
+        check(self._lib.hmmbw_set_option(self._ctx, OPT_LIVE_STATUS, 1 if on else 0))
+
+    def wait_live(self, iterations: int, first: int = 0,
+                  count: int = 0) -> Tuple[Status, List[Tuple[float, float]]]:
+        """Wait (polling the host mirror, no stream sync) until `iterations` EM iterations are recorded or EM
+        stopped; status + the records [first, first+count)."""
+        st = Status()
+        recs = (IterRecord * max(count, 1))()
+        check(self._lib.hmmbw_status_live_wait(self._ctx, int(iterations), ctypes.byref(st),
+                                               ctypes.cast(recs, ctypes.c_void_p) if count else None,
+                                               int(first), int(count)))
+        return st, [(recs[i].log_likelihood, recs[i].diff) for i in range(count)]
 
     def wait_status(self, ticket: int, first: int = 0) -> Tuple[Status, List[Tuple[float, float]]]:
         """Wait for snapshot `ticket` only (not for the work queued after it): status + records [first, ...)."""

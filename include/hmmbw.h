@@ -32,8 +32,9 @@
 extern "C" {
 #endif
 
-#define HMMBW_ABI_VERSION 3 /* 2: hmmbw_iterate_begin/_end, status snapshots, comm info/payload;
-                              3: peer all-reduce (hmmbw_peer_*), HMMBW_E_TIMEOUT, cache trim, split timing */
+#define HMMBW_ABI_VERSION 4 /* 2: hmmbw_iterate_begin/_end, status snapshots, comm info/payload;
+                              3: peer all-reduce (hmmbw_peer_*), HMMBW_E_TIMEOUT, cache trim, split timing;
+                              4: live status mirror (HMMBW_OPT_LIVE_STATUS, hmmbw_status_live_wait) */
 
 #define HMMBW_OK 0
 #define HMMBW_E_INVALID (-1)        /* bad argument (shape, range, null pointer)             */
@@ -205,6 +206,17 @@ int hmmbw_status_post(hmmbw_ctx *ctx, int64_t first, int64_t *ticket);
 int hmmbw_status_wait(hmmbw_ctx *ctx, int64_t ticket, hmmbw_status *status, hmmbw_iter_record *records,
                       int64_t first, int64_t count);
 
+/* With HMMBW_OPT_LIVE_STATUS = 1 every M-step that records an iteration (:503-514) also writes that
+ * record and the new status into pinned host memory from the device, while the launch that runs it (with
+ * merged M-steps: the next E-step, in its prologue) is still executing.  This waits, by polling that
+ * memory, until `iterations` iterations are recorded or EM has stopped, then fills status and the records
+ * [first, first+count).  No stream synchronisation and no extra kernel: a host loop sees iteration e's
+ * convergence record a few microseconds into launch e + 1, while launch e + 2 can already be queued
+ * behind it (the reference's per-iteration check, :346,503-514, without idling the GPU).  If the stream
+ * runs dry first (the last M-step still pending, or a device-side stop), it returns the device status. */
+int hmmbw_status_live_wait(hmmbw_ctx *ctx, int64_t iterations, hmmbw_status *status, hmmbw_iter_record *records,
+                           int64_t first, int64_t count);
+
 /* SYNC. Current parameters.  normalise=1 applies the reference's return path (safe_exp then
  * pi/sum(pi), row-normalise A and B rows with positive sums, :524-541); normalise=0 returns the
  * unnormalised working parameters (exp of the reference's log_pi/log_a/log_b matrices). */
@@ -247,6 +259,9 @@ int hmmbw_score(hmmbw_ctx *ctx, double *out);
 /* Bound, in milliseconds, of the peer all-reduce's device-side wait for the other ranks' statistics
  * (default 30000).  Past it the iteration fails with HMMBW_E_TIMEOUT instead of spinning. */
 #define HMMBW_OPT_PEER_TIMEOUT_MS 9
+/* 1: keep a host mirror of the convergence state that the M-steps update (hmmbw_status_live_wait);
+ * 0 (default): off.  Synchronises the context stream when changed. */
+#define HMMBW_OPT_LIVE_STATUS 10
 int hmmbw_set_option(hmmbw_ctx *ctx, int key, int64_t value);
 
 /* E-step kernel timing with HIP events on the context stream (for bench/roofline).  Returns the

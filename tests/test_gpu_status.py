@@ -75,3 +75,40 @@ def test_pipelined_train_reports_every_iteration_once(oracle, max_it, eps):
     assert st.iterations == len(ref.trace_L)
     np.testing.assert_allclose([L for _, L, _ in seen], ref.trace_L, rtol=1e-9)
     assert bool(st.converged) == (st.iterations < max_it)
+
+
+@pytest.mark.parametrize("merge", [True, False])
+def test_live_mirror_matches_sync_records_and_resets(merge):
+    """HMMBW_OPT_LIVE_STATUS: the records the M-steps mirror into pinned host memory are the numbers a
+    synchronous hmmbw_get_status returns; a wait for more iterations than the queued launches can record
+    falls back to the device status once the stream is idle; after a reset the previous run's mirror
+    no longer satisfies a wait."""
+    e, _, _ = _engine(8, 64, 400, 9, merge)
+    with e:
+        e.live_status(True)
+        e.reset(0.0, 100)
+        e.enqueue_iterations(6)
+        # merged: launch e + 1 records iteration e, so 6 launches record 5 before the final flush
+        want = 5 if merge else 6
+        st, recs = e.wait_live(want, 0, want)
+        assert st.iterations == want and not st.done
+        # nothing will record a 7th iteration: the wait returns the device status when the stream drains
+        st2, _ = e.wait_live(want + 3)
+        assert st2.iterations == want
+        stf, recsf = e.status(0, 6)  # synchronous, flushes the pending M-step
+        assert recs == recsf[:want]
+        # a new run: the mirror of the old one (6 iterations) must not satisfy a wait for 2
+        e.reset(0.0, 100)
+        e.enqueue_iterations(3)
+        st3, recs3 = e.wait_live(2, 0, 2)
+        assert st3.iterations == 2
+        st4, recs4 = e.status(0, 3)
+        assert recs3 == recs4[:2]
+        # stop rule: max_iterations = 4 on a fresh run, more launches than that queued
+        e.reset(0.0, 4)
+        e.enqueue_iterations(8)
+        st5, _ = e.wait_live(100)
+        assert st5.done and st5.iterations == 4
+        e.live_status(False)
+        with pytest.raises(Exception):
+            e.wait_live(1)

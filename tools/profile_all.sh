@@ -1,22 +1,30 @@
 #!/bin/bash
 # Refresh every profile of one round on the GPU box (run from the repo root):
-#   bash tools/profile_all.sh <tag>
+#   bash tools/profile_all.sh <tag> [part]
+# part: all (default), a (calibration + the cfg3 workloads) or b (cfg5, cfg4 shard, cfg2, vq, bench lines):
+# the halves fit one gpurun call each
 # rocprofv3 kernel trace + stats per workload, then separate PMC passes (never combined with a
 # trace domain): FETCH_SIZE, WRITE_SIZE (HBM traffic, corrected by the tools/pmc_calib.hip run) and an
 # SQ/LDS pass (bank conflicts, VALU/LDS instruction counts), plus the bench JSON lines.
 set -uo pipefail
 TAG=${1:-r2}
+PART=${2:-all}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 step() { echo "[$(date +%T)] $*"; }
-hipcc --offload-arch=gfx950 -O3 -o "$OUT/pmc_calib" "$R/tools/pmc_calib.hip" || exit 1
 cd /tmp
+WLS="lr_cfg3 lrH_cfg3 dense_cfg3 cfg5 cfg4shard"
+[ "$PART" = a ] && WLS="lr_cfg3 lrH_cfg3 dense_cfg3"
+[ "$PART" = b ] && WLS="cfg5 cfg4shard"
+if [ "$PART" != b ]; then
+hipcc --offload-arch=gfx950 -O3 -o "$OUT/pmc_calib" "$R/tools/pmc_calib.hip" || exit 1
 for C in FETCH_SIZE WRITE_SIZE; do
   step calib $C
   timeout -k 10 120 rocprofv3 --pmc $C --output-format csv -d "$OUT/calib_$C" -o run -- "$OUT/pmc_calib" > "$OUT/calib_$C.log" 2>&1 || exit 1
 done
+fi
 SQ="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE"
 # instruction mix: fp64 VALU issues over 4 cycles on a SIMD-32, the rest over 2 (MI355X_MICROARCH.md); fp64 MFMA busy
 SQ2="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU_MFMA_F64 SQ_VALU_MFMA_BUSY_CYCLES"
@@ -27,7 +35,7 @@ declare -A ARGS=(
   [cfg5]="--steps 5 --warmup 2 --no-cpu-baseline --no-synced --workload cfg5"
   [cfg4shard]="--steps 20 --warmup 3 --no-cpu-baseline --no-synced --workload cfg4"
 )
-for W in lr_cfg3 lrH_cfg3 dense_cfg3 cfg5 cfg4shard; do
+for W in $WLS; do
   BENCH="$R/bench.py ${ARGS[$W]}"
   step trace $W
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace_$W" -o run -- python3 $BENCH > "$OUT/bench_trace_$W.log" 2>&1 || exit 1
@@ -40,6 +48,7 @@ for W in lr_cfg3 lrH_cfg3 dense_cfg3 cfg5 cfg4shard; do
   step pmc SQ2 $W
   timeout -k 10 300 rocprofv3 --pmc $SQ2 --output-format csv -d "$OUT/pmc_SQ2_$W" -o run -- python3 $BENCH > "$OUT/bench_pmc_SQ2_$W.log" 2>&1 || exit 1
 done
+[ "$PART" = a ] && { step done; exit 0; }
 step trace cfg2
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace_cfg2" -o run -- python3 $R/tools/bench_cfg2.py --no-cpu > "$OUT/bench_cfg2.log" 2>&1 || exit 1
 step trace vq
