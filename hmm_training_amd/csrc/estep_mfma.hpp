@@ -44,6 +44,8 @@ constexpr int kTileSeqs = 16;  // sequences per tile = MFMA columns
 // counted vmcnt waits (the join points after such branches drain every prefetch with vmcnt(0)).
 #ifdef HMMBW_WIDE_ABLATE
 #define WIDE_ABL(a, bit) (((a).ablate & (bit)) != 0)
+#elif defined(HMMBW_WIDE_ABLATE_CT)  // compile-time mask: the ablated build keeps the release schedule
+#define WIDE_ABL(a, bit) ((HMMBW_WIDE_ABLATE_CT & (bit)) != 0)
 #else
 #define WIDE_ABL(a, bit) false
 #endif
@@ -83,6 +85,7 @@ __global__ void __launch_bounds__(NT * 64, 2) k_estep_mfma(EArgs a) {  // 2 wave
              i += (long long)gridDim.x * blockDim.x)
             a.zero[i] = 0.0;
     if (a.state != nullptr && a.state->done) return;    // converged: device-side no-op (:346)
+    CHUNKSTAMP(0, 62);  // diagnostics build only (tools/wide_chunk_times.py): shader-clock stamps per chunk
     const int tid = threadIdx.x, lane = tid & 63, m = tid >> 6;
     const int s = lane & 15, g = lane >> 4;
     const int N = a.N;
@@ -97,10 +100,11 @@ __global__ void __launch_bounds__(NT * 64, 2) k_estep_mfma(EArgs a) {  // 2 wave
     double *ckw = a.ckpt + (FWD_ONLY ? 0 : a.L.wave_ckoff[tile]) + (long long)m * 4 * 64 + lane;
     int *ew = a.ebuf + (FWD_ONLY ? 0 : a.L.wave_spoff[tile]) + s;
     const int col0 = 16 * m + 4 * g;  // this lane's 4 emission columns (bt_col order)
-    // gamma row of position (t, s): gw + t * 16 * NP, this lane's 4 columns
-    double *gw = a.gam + (FWD_ONLY ? 0 : a.L.wave_ckoff[tile]) + (long long)s * NP + col0;
-    auto putg = [&](int t, const f64x4 &v) HMMBW_AI {
-        double2 *q = reinterpret_cast<double2 *>(gw + (long long)t * kTileSeqs * NP);
+    // gamma row of position (t, s): row gdw[t * 16] of the symbol-sorted row buffer (the host's
+    // position -> rank map), so that k_bnum_gather streams each symbol's rows contiguously
+    const unsigned *gdw = a.gdst + (FWD_ONLY ? 0 : a.L.wave_ckoff[tile] / NP) + s;
+    auto putg = [&](unsigned row, const f64x4 &v) HMMBW_AI {
+        double2 *q = reinterpret_cast<double2 *>(a.gam + (long long)row * NP + col0);
         q[0] = double2{v[0], v[1]};
         q[1] = double2{v[2], v[3]};
     };
@@ -213,6 +217,7 @@ __global__ void __launch_bounds__(NT * 64, 2) k_estep_mfma(EArgs a) {  // 2 wave
     uint4 p0, p1;  // symbol packs of chunks c and c + 1
     auto fchunk = [&](int c, auto MASK_, auto STEADY_) HMMBW_AI {
         constexpr bool STEADY = decltype(STEADY_)::value;
+        CHUNKSTAMP(0, c);
         const uint4 p2 = loadpack(c + 2 < nch ? c + 2 : nch - 1);
 #pragma unroll
         for (int k = 0; k < kChunk; ++k) {
@@ -238,6 +243,7 @@ __global__ void __launch_bounds__(NT * 64, 2) k_estep_mfma(EArgs a) {  // 2 wave
     if (full) forward(std::false_type{});
     else forward(std::true_type{});
 
+    CHUNKSTAMP(0, 61);
     // log P(O|lambda) = log(sum_j z_{T-1}(j)) + ln2 * C   (:375-377)
     double ps = (z[0] + z[1]) + (z[2] + z[3]);
     ps += __shfl_xor(ps, 16);
@@ -262,7 +268,7 @@ __global__ void __launch_bounds__(NT * 64, 2) k_estep_mfma(EArgs a) {  // 2 wave
             f64x4 gT;
 #pragma unroll
             for (int r = 0; r < 4; ++r) gT[r] = z[r] * inv_p;
-            if (T > 0 && !WIDE_ABL(a, 4)) putg(T - 1, gT);
+            if (T > 0 && !WIDE_ABL(a, 4)) putg(gdw[(T - 1) * kTileSeqs], gT);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int j = 16 * m + g + 4 * r;
@@ -292,6 +298,7 @@ __global__ void __launch_bounds__(NT * 64, 2) k_estep_mfma(EArgs a) {  // 2 wave
         // loaded one visit before
         f64x4 zring[2], bring1[2];
         int sring[2];
+        unsigned dring[2];  // gamma row of step t in slot t % 2, loaded in the visit before consume(t)
         f64x4 zs;  // z_t masked to the regular steps: gamma_t of the step that consumes the image
         auto ldz = [&](int t) HMMBW_AI -> f64x4 {
             f64x4 v;
@@ -324,7 +331,7 @@ __global__ void __launch_bounds__(NT * 64, 2) k_estep_mfma(EArgs a) {  // 2 wave
         // to follow it (a register dependency on beta_t), so that the next step's image is computed
         // and published (VALU, LDS writes) between them instead of after them, and the wave reaches
         // the next barrier right after its last MFMA issues.
-        auto consume = [&](int t, auto MASK_, auto STEADY_, auto &&next) HMMBW_AI {
+        auto consume = [&](int t, unsigned grow, auto MASK_, auto STEADY_, auto &&next) HMMBW_AI {
             constexpr bool MASK = decltype(MASK_)::value;
             constexpr bool STEADY = decltype(STEADY_)::value;
             const bool reg = !MASK || t <= T - 2;
@@ -353,7 +360,7 @@ __global__ void __launch_bounds__(NT * 64, 2) k_estep_mfma(EArgs a) {  // 2 wave
             for (int kk = 0; kk < 4; ++kk)
 #pragma unroll
                 for (int mj = 0; mj < NT; ++mj) S[mj] = mfma_f64(za[kk], tsrc[16 * mj * kXs + 4 * kk], S[mj]);
-            if ((!MASK || reg) && !WIDE_ABL(a, 4)) putg(t, gm);  // B numerator row (:474-485)
+            if ((!MASK || reg) && !WIDE_ABL(a, 4)) putg(grow, gm);  // B numerator row (:474-485)
             if (!STEADY && t == 0) {  // pi_num (:415-420): gamma_0 summed over the tile's sequences
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
@@ -370,6 +377,7 @@ __global__ void __launch_bounds__(NT * 64, 2) k_estep_mfma(EArgs a) {  // 2 wave
         // from slot t % 2), then b(o_{t-1}), s_{t-1} and alpha_hat_{t-3} into the slots just consumed
         auto bchunk = [&](int c, auto MASK_, auto STEADY_) HMMBW_AI {
             constexpr bool STEADY = decltype(STEADY_)::value;  // c >= 1 and every step t <= Tw - 2
+            CHUNKSTAMP(1, c);
             const uint4 pp = loadpack(c >= 1 ? c - 1 : 0);
 #pragma unroll
             for (int k = kChunk - 1; k >= 0; --k) {
@@ -379,8 +387,9 @@ __global__ void __launch_bounds__(NT * 64, 2) k_estep_mfma(EArgs a) {  // 2 wave
                         publish(t - 1, zring[(k + 1) & 1], bring1[k & 1], sring[k & 1], MASK_);
                 };
                 // tile-uniform; gamma_{T-1} is done above
-                if (STEADY || t <= Tw - 2) consume(t, MASK_, STEADY_, pub);
+                if (STEADY || t <= Tw - 2) consume(t, dring[k & 1], MASK_, STEADY_, pub);
                 else pub();
+                if (STEADY || t >= 1) dring[(k + 1) & 1] = gdw[(t - 1) * kTileSeqs];  // row of step t - 1
                 if (STEADY || t >= 2) {
                     bring1[(k + 1) & 1] = emis(k >= 1 ? sym_of(pc, k - 1) : sym_of(pp, kChunk - 1));  // b(o_{t-1})
                     sring[(k + 1) & 1] = ew[(t - 1) * kTileSeqs];                                   // s_{t-1}
@@ -401,6 +410,7 @@ __global__ void __launch_bounds__(NT * 64, 2) k_estep_mfma(EArgs a) {  // 2 wave
             // b(o_{ttop-1}), s_{ttop-1} for the first visit (slot 1: ttop - 1 is odd)
             bring1[1] = emis(sym_of(pc, kChunk - 1));
             sring[1] = ew[(ttop - 1) * kTileSeqs];
+            dring[1] = gdw[(ttop - 1) * kTileSeqs];
             // chunks [1, cs] have every step t <= Tw - 2 (c * kChunk + kChunk - 1 <= Tw - 2)
             const int cs = Tw >= kChunk + 1 ? (Tw - kChunk - 1) / kChunk : 0;
             int c = nch - 1;
@@ -410,6 +420,7 @@ __global__ void __launch_bounds__(NT * 64, 2) k_estep_mfma(EArgs a) {  // 2 wave
         };
         if (full) backward(std::false_type{});
         else backward(std::true_type{});
+        CHUNKSTAMP(1, 62);
         // ---- flush: xi = a_ij S_ij; gamma sums reduced over the tile's sequences ----
         double *part = DET ? a.part + (long long)blockIdx.x * a.off_bnum : nullptr;
 #pragma unroll
@@ -452,6 +463,7 @@ __global__ void __launch_bounds__(NT * 64, 2) k_estep_mfma(EArgs a) {  // 2 wave
             if ((threadIdx.x >> 6) == 0 && __shfl(ticket, 0) == (int)(gridDim.x - 1)) rank_ll_fold(a, gridDim.x);
         }
     }
+    CHUNKSTAMP(1, 63);
 }
 
 // B numerator of the wide kernels (:474-485): B_num[k][j] = sum of the gamma rows of every position
@@ -463,6 +475,9 @@ __global__ void __launch_bounds__(NT * 64, 2) k_estep_mfma(EArgs a) {  // 2 wave
 // positions in list order, the four waves in wave order), plain stores into the symbol-major [K][N]
 // statistics block.  Also the small kernels' deterministic mode (NP = G columns in state order,
 // perm = 0).  Round 3: 234.5 us at the cfg5 shard against 237.0 for one index load per 4 rows.
+// SORTED (the wide path): the E-step wrote every position's row at its rank in symbol order, so symbol k's
+// rows are the contiguous rows [ptr[k], ptr[k+1]) and the walk is a stream (no row index to load).
+template <bool SORTED>
 __global__ void __launch_bounds__(256) k_bnum_gather(const double *gam, const unsigned *rows, const long long *ptr,
                                                        int NP, int N, int perm, double *bnum, const IterState *state) {
     __shared__ double sh[4][64];
@@ -473,21 +488,21 @@ __global__ void __launch_bounds__(256) k_bnum_gather(const double *gam, const un
     constexpr int U = 16;
     auto ldidx = [&](long long p0) -> unsigned {
         const long long p = p0 + 64 * wv + lane;
-        return rows[p < e ? p : b];
+        return SORTED ? 0u : rows[p < e ? p : b];
     };
     double acc = 0.0;
     unsigned idx = b < e ? ldidx(b) : 0u;
     for (long long p0 = b; p0 < e; p0 += 256) {
         const unsigned cur = idx;
-        if (p0 + 256 < e) idx = ldidx(p0 + 256);
+        if (!SORTED && p0 + 256 < e) idx = ldidx(p0 + 256);
         const long long pw = p0 + 64 * wv;  // this wave's first position of the batch
 #pragma unroll
         for (int g = 0; g < 64; g += U) {
             double x[U];
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-                const unsigned r = __builtin_amdgcn_readlane(cur, g + u);
-                x[u] = gam[(long long)r * NP + q];
+                const long long r = SORTED ? (pw + g + u < e ? pw + g + u : b) : (long long)__builtin_amdgcn_readlane(cur, g + u);
+                x[u] = gam[r * NP + q];
             }
 #pragma unroll
             for (int u = 0; u < U; ++u) acc += (pw + g + u < e) ? x[u] : 0.0;

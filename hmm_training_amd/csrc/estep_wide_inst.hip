@@ -13,6 +13,18 @@ Kernels wide_kernels(int NP) {
     return k;
 }
 
-BnumFn bnum_gather_kernel() { return k_bnum_gather; }
+BnumFn bnum_gather_kernel(bool sorted) { return sorted ? k_bnum_gather<true> : k_bnum_gather<false>; }
 
 }  // namespace hmmbw
+
+#if defined(HMMBW_PHASE_TIMES) && defined(HMMBW_CHUNK_TIMES)
+// Diagnostics build: the wide kernel's chunk stamps live in this unit's device module.
+extern "C" int hmmbw_debug_wide_chunk_times(unsigned long long *out, int64_t nwaves) {
+    using namespace hmmbw;
+    if (!out || nwaves < 0 || nwaves > 4096) return -1;
+    if (hipDeviceSynchronize() != hipSuccess) return -2;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_chunk), sizeof(unsigned long long) * 128 * nwaves) != hipSuccess)
+        return -2;
+    return 0;
+}
+#endif

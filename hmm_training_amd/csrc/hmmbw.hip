@@ -471,7 +471,7 @@ struct hmmbw_ctx {
     long long nblocks = 0;
     long long nfull = 0;          // small kernels: workgroups with 4 active waves (then xact-wave ones)
     int xact = 4;
-    int prio = 0;                 // diagnostics: HMMBW_PRIO at set_observations (see EArgs::prio)
+    int prio = 2;                 // wave priority of the small kernels (EArgs::prio); HMMBW_PRIO overrides it
     uint16_t *d_sym = nullptr;
     long long *d_wsym = nullptr, *d_wckoff = nullptr, *d_wspoff = nullptr;
     int *d_wT = nullptr, *d_wfull = nullptr, *d_slen = nullptr, *d_sseq = nullptr;
@@ -617,6 +617,7 @@ EArgs make_eargs(hmmbw_ctx *c) {
     a.Bt = c->d_Bt;
     a.ckpt = c->d_ck;
     a.gam = c->d_gam;
+    a.gdst = c->wide ? c->d_brows : nullptr;
     a.part = c->d_part;
     a.spack = c->d_sp;
     a.ebuf = c->d_ebuf;
@@ -818,14 +819,14 @@ int launch_estep(hmmbw_ctx *c, bool fwd_only, const IterState *state, double *co
             hipLaunchKernelGGL(k_det_reduce, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, c->stream, c->d_part,
                                (long long)p.grid, n, a.copies, a.state);
         }
-        hipLaunchKernelGGL(bnum_gather_kernel(), dim3((unsigned)c->K), dim3(256), 0, c->stream, c->d_gam,
-                           c->d_brows, c->d_bptr, c->NP, c->N, 1, a.copies + c->off_bnum(), a.state);
+        hipLaunchKernelGGL(bnum_gather_kernel(true), dim3((unsigned)c->K), dim3(256), 0, c->stream, c->d_gam,
+                           nullptr, c->d_bptr, c->NP, c->N, 1, a.copies + c->off_bnum(), a.state);
         HIP_TRY(hipGetLastError());
     } else if (c->det && !fwd_only) {  // deterministic mode: fixed-order sums of the partials and gamma rows
         const long long n = c->off_bnum();
         hipLaunchKernelGGL(k_det_reduce, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, c->stream, c->d_part,
                            (long long)p.grid, n, a.copies, a.state);
-        hipLaunchKernelGGL(bnum_gather_kernel(), dim3((unsigned)c->K), dim3(256), 0, c->stream, c->d_gam,
+        hipLaunchKernelGGL(bnum_gather_kernel(false), dim3((unsigned)c->K), dim3(256), 0, c->stream, c->d_gam,
                            c->d_brows, c->d_bptr, c->G, c->N, 0, a.copies + c->off_bnum(), a.state);
         HIP_TRY(hipGetLastError());
     }
@@ -1215,23 +1216,28 @@ int hmmbw_set_observations(hmmbw_ctx *c, const int64_t *offsets, const int32_t *
     }
     std::vector<long long> bptr;
     std::vector<unsigned> brows;
-    if (c->wide) {  // symbol -> gamma-row index (row = tile offset / NP + t * 16 + u), symbol order stable
+    if (c->wide) {
+        // position -> its row in symbol order (positions of one symbol in tile-row order): the E-step writes
+        // the gamma row of tile row wck / NP + t * 16 + u there (brows, indexed by tile row), so symbol k's
+        // rows are [bptr[k], bptr[k+1]) and k_bnum_gather streams them
         if (cktot / c->NP >= (1LL << 32)) return fail(HMMBW_E_UNSUPPORTED, "too many positions for the wide path");
         bptr.assign((size_t)c->K + 1, 0);
         for (int64_t i = 0; i < total; ++i) ++bptr[(size_t)symbols[i] + 1];
         for (int k = 0; k < c->K; ++k) bptr[(size_t)k + 1] += bptr[(size_t)k];
         std::vector<long long> fill(bptr.begin(), bptr.end() - 1);
-        brows.resize((size_t)std::max<int64_t>(total, 1));
+        // rows of padding slots (a tile's slots past the last sequence: full-tile code paths store their
+        // exact-zero gamma rows unmasked) all go to one scratch row past the real ones
+        brows.assign((size_t)std::max(cktot / c->NP, 1LL), (unsigned)total);
         for (long long w = 0; w < nwaves; ++w)
             for (int u = 0; u < U; ++u) {
                 const long long sl = w * U + u;
                 if (sl >= R) continue;
                 const int64_t r = perm[(size_t)sl];
                 for (int t = 0; t < len[(size_t)r]; ++t)
-                    brows[(size_t)fill[(size_t)symbols[offsets[r] + t]]++] =
-                        (unsigned)(wck[(size_t)w] / c->NP + (long long)t * U + u);
+                    brows[(size_t)(wck[(size_t)w] / c->NP + (long long)t * U + u)] =
+                        (unsigned)fill[(size_t)symbols[offsets[r] + t]]++;
             }
-        if (!rc) rc = dalloc(&c->d_gam, (size_t)std::max(cktot, 1LL));
+        if (!rc) rc = dalloc(&c->d_gam, (size_t)(total + 1) * c->NP);
         if (!rc) rc = dalloc(&c->d_bptr, bptr.size());
         if (!rc) rc = dalloc(&c->d_brows, brows.size());
         if (!rc && c->det) rc = dalloc(&c->d_part, (size_t)std::max(nblocks, 1LL) * (size_t)c->off_bnum());

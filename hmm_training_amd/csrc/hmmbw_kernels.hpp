@@ -30,7 +30,7 @@ Kernels wide_kernels(int NP);
 
 // The wide path's B-numerator gather (estep_mfma.hpp).
 using BnumFn = void (*)(const double *, const unsigned *, const long long *, int, int, int, double *, const IterState *);
-BnumFn bnum_gather_kernel();
+BnumFn bnum_gather_kernel(bool sorted);  // sorted: the wide path's symbol-ordered rows
 
 // The VQ encoder (vq.hip).
 hipError_t launch_vq(hipStream_t st, const double *frames, long long n_frames, int stride, int col0, int dims,
