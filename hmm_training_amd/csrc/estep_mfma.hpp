@@ -75,11 +75,13 @@ __device__ __forceinline__ f64x4 mfma_f64(double a, double b, f64x4 c) {
 template <int NT, bool FWD_ONLY, bool DET = false>
 __global__ void __launch_bounds__(NT * 64, 2) k_estep_mfma(EArgs a) {  // 2 waves per SIMD: <= 256 VGPRs
     static_assert(!(DET && FWD_ONLY), "deterministic mode is an E-step option");
-    constexpr int NP = 16 * NT, KB = 4 * NT, IMG = NP * kXs;
+    constexpr int NP = 16 * NT, KB = 4 * NT, IMG = NP * kXs, IMGX = 2 * IMG;
     extern __shared__ __attribute__((aligned(256))) double smem[];  // 256-B aligned whatever the static LDS (ds_read_b128 rows)
-    double *X0 = smem;                                   // [2][NP][kXs]: z (forward) / V (backward)
-    // smem + 2 * IMG: [2][NP][kXs] masked z (backward xi operand), addressed as putb / topb + 2 * IMG
-    double *sRed = smem + (FWD_ONLY ? 2 : 4) * IMG;      // [NT][16] partial sums + block LL scratch
+    // [2][2 NP][kXs]: z (forward) / v (backward) images, every row stored twice (rows r and r + NP), so that
+    // wave m reads the other blocks in the order 16m + 16, ..., 16m + NP - 1 without wrapping (below)
+    double *X0 = smem;
+    double *Z0 = smem + 2 * IMGX;                        // [2][NP][kXs] masked z (backward xi operand)
+    double *sRed = smem + (FWD_ONLY ? 2 * IMGX : 2 * IMGX + 2 * IMG);  // [NT][16] partial sums + block LL scratch
     if constexpr (!FWD_ONLY)  // clear the next iteration's statistics (single rank: triple buffer)
         for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < a.zero_len;
              i += (long long)gridDim.x * blockDim.x)
@@ -117,15 +119,28 @@ __global__ void __launch_bounds__(NT * 64, 2) k_estep_mfma(EArgs a) {  // 2 wave
         const double2 lo = p[0], hi = p[1];
         return f64x4{lo.x, lo.y, hi.x, hi.y};
     };
-    // this wave's block of a [state][16] LDS image (C/D form), the B operand of k-block kb, and the
-    // transposed read [state 16mm + (lane & 15)][sequence 4kk + (lane >> 4)] (the xi operands)
-    double *const putb = X0 + (16 * m + g) * kXs + s;
-    auto put = [&](double *base, int p, const f64x4 &v) HMMBW_AI {
+    // Own block first.  The recursions contract over all NP states in k-blocks of 4, and the C/D registers
+    // of this wave's block ARE the B operands of its own 4 k-blocks (4m + r: states 16m + 4r + g), so each
+    // step issues those 4 MFMAs straight from registers BEFORE the barrier and the LDS reads of the other
+    // waves' blocks, which the wave reads in the rotated order 16m + 16, ..., 16m + NP - 1 (mod NP, hence
+    // the doubled image rows); the A operands are loaded in the same rotated k-block order.  That hides
+    // part of the exchange (LDS write, barrier, LDS read) behind matrix work.
+    double *const putb = X0 + (16 * m + g) * kXs + s;   // this wave's block, both copies
+    auto put2 = [&](int p, const f64x4 &v) HMMBW_AI {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) base[p * IMG + 4 * r * kXs] = v[r];
+        for (int r = 0; r < 4; ++r) {
+            putb[p * IMGX + 4 * r * kXs] = v[r];
+            putb[p * IMGX + NP * kXs + 4 * r * kXs] = v[r];
+        }
     };
-    const double *const bopb = X0 + g * kXs + s;
+    double *const putz = Z0 + (16 * m + g) * kXs + s;
+    auto putzs = [&](int p, const f64x4 &v) HMMBW_AI {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) putz[p * IMG + 4 * r * kXs] = v[r];
+    };
+    const double *const bopr = X0 + (16 * m + g) * kXs + s;  // + 4 kb' kXs: rotated k-block kb' (>= 4) of image p
     const double *const topb = X0 + (lane & 15) * kXs + (lane >> 4);
+    const double *const topz = Z0 + (lane & 15) * kXs + (lane >> 4);
     auto bexp = [](double x) HMMBW_AI -> int { return (int)__builtin_amdgcn_ubfe((unsigned)__double2hiint(x), 20, 11); };
     // sum over the 16 sequences of a 16-lane row
     auto rowsum = [](double x) HMMBW_AI -> double {
@@ -136,10 +151,10 @@ __global__ void __launch_bounds__(NT * 64, 2) k_estep_mfma(EArgs a) {  // 2 wave
 
     // forward A operands of this wave's 16-state block: A^T[o][i] = a_io (o = 16m + (lane&15),
     // i = 4kb + (lane>>4))
-    double aop[KB];
+    double aop[KB];  // rotated k-block order: aop[kb'] is k-block (kb' + 4m) mod KB
 #pragma unroll
     for (int kb = 0; kb < KB; ++kb) {
-        const int o = 16 * m + (lane & 15), i = 4 * kb + (lane >> 4);
+        const int o = 16 * m + (lane & 15), i = 4 * ((kb + 4 * m) % KB) + (lane >> 4);
         aop[kb] = (i < N && o < N) ? a.A[i * N + o] : 0.0;
     }
 
@@ -164,27 +179,36 @@ __global__ void __launch_bounds__(NT * 64, 2) k_estep_mfma(EArgs a) {  // 2 wave
                 x[r] = (j < N && T > 0) ? a.pi[j] * b[r] : 0.0;  // pi_j b_j(o_0) (:357-360)
             }
         } else {
-            const double *src = bopb + ((t - 1) & 1) * IMG;
-            double zb[KB];
-#pragma unroll
-            for (int kb = 0; kb < KB; ++kb) zb[kb] = src[4 * kb * kXs];
             // one accumulation chain: a dependent v_mfma_f64_16x16x4 issues every 64 cycles, its full
-            // rate (tools/ubench_mfma.hip), and a second chain would cost 8 VGPRs
+            // rate (tools/ubench_mfma.hip), and a second chain would cost 8 VGPRs.  Own block first, from
+            // the registers (z = z_{t-1}), then the barrier after which the other waves' z_{t-1} is readable
             f64x4 acc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-            for (int kb = 0; kb < KB; ++kb) acc = mfma_f64(aop[kb], zb[kb], acc);
+            for (int r = 0; r < 4; ++r) acc = mfma_f64(aop[r], z[r], acc);
+            // keep the own-block MFMAs in front of the barrier (they touch no memory, so the scheduler would
+            // move them behind it, and the LDS reads behind them)
+            __builtin_amdgcn_sched_barrier(0);
+            if (!WIDE_ABL(a, 16)) __syncthreads();
+            const double *src = bopr + ((t - 1) & 1) * IMGX;
+            double zb[KB];
+#pragma unroll
+            for (int kb = 4; kb < KB; ++kb) zb[kb] = src[4 * kb * kXs];
+#pragma unroll
+            for (int kb = 4; kb < KB; ++kb) acc = mfma_f64(aop[kb], zb[kb], acc);
             // s_t from z_{t-1} over all NP states of the sequence (4 lanes x KB values)
             int M = 0;
 #pragma unroll
-            for (int kb = 0; kb < KB; ++kb) M = max(M, bexp(zb[kb]));
+            for (int r = 0; r < 4; ++r) M = max(M, bexp(z[r]));
+#pragma unroll
+            for (int kb = 4; kb < KB; ++kb) M = max(M, bexp(zb[kb]));
             // across the 4 lane rows: gfx950's row-swap permutes are VALU ops (ds_bpermute put two LDS
             // round trips in front of the MFMA chain, which the compiler schedules after them)
             M = row_max4(M);
             // the exponent's VALU work between the chain's MFMAs (each waits ~64 cycles for the last)
             // instead of in front of the first one
-            __builtin_amdgcn_sched_group_barrier(0x100, KB / 2, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, (KB - 4) / 2, 0);
 #pragma unroll
-            for (int kb = 0; kb < KB; ++kb) {
+            for (int kb = 4; kb < KB; ++kb) {
                 __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
                 __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
             }
@@ -202,7 +226,7 @@ __global__ void __launch_bounds__(NT * 64, 2) k_estep_mfma(EArgs a) {  // 2 wave
             z = x;
         }
         C += sc;
-        put(putb, t & 1, z);
+        put2(t & 1, z);
         if constexpr (!FWD_ONLY) {
             if (!WIDE_ABL(a, 8)) {
 #pragma unroll
@@ -212,7 +236,7 @@ __global__ void __launch_bounds__(NT * 64, 2) k_estep_mfma(EArgs a) {  // 2 wave
             // lanes, the same value to the same 16 words, so the store needs no exec branch)
             if (STEADY || (m == 0 && g == 0)) ew[t * kTileSeqs] = sc;
         }
-        if (!WIDE_ABL(a, 16)) __syncthreads();
+        // no barrier here: the next step issues its own-block MFMAs first (above)
     };
     uint4 p0, p1;  // symbol packs of chunks c and c + 1
     auto fchunk = [&](int c, auto MASK_, auto STEADY_) HMMBW_AI {
@@ -284,8 +308,8 @@ __global__ void __launch_bounds__(NT * 64, 2) k_estep_mfma(EArgs a) {  // 2 wave
         }
         // backward A operands A[i][j] (i = 16m + (lane&15), j = 4kb + (lane>>4))
 #pragma unroll
-        for (int kb = 0; kb < KB; ++kb) {
-            const int i = 16 * m + (lane & 15), jj = 4 * kb + (lane >> 4);
+        for (int kb = 0; kb < KB; ++kb) {  // rotated k-block order, as the forward's
+            const int i = 16 * m + (lane & 15), jj = 4 * ((kb + 4 * m) % KB) + (lane >> 4);
             aop[kb] = (i < N && jj < N) ? a.A[i * N + jj] : 0.0;
         }
         f64x4 beta = {inv_p, inv_p, inv_p, inv_p};
@@ -300,6 +324,7 @@ __global__ void __launch_bounds__(NT * 64, 2) k_estep_mfma(EArgs a) {  // 2 wave
         int sring[2];
         unsigned dring[2];  // gamma row of step t in slot t % 2, loaded in the visit before consume(t)
         f64x4 zs;  // z_t masked to the regular steps: gamma_t of the step that consumes the image
+        f64x4 accn;  // beta of the next step to consume: its own-block MFMAs, issued by publish
         auto ldz = [&](int t) HMMBW_AI -> f64x4 {
             f64x4 v;
             if (WIDE_ABL(a, 8)) return f64x4{0.5, 0.5, 0.5, 0.5};
@@ -323,8 +348,12 @@ __global__ void __launch_bounds__(NT * 64, 2) k_estep_mfma(EArgs a) {  // 2 wave
                     zs[r] = zt[r];
                 }
             }
-            put(putb, t & 1, v);
-            put(putb + 2 * IMG, t & 1, zs);
+            put2(t & 1, v);
+            putzs(t & 1, zs);
+            // the own-block part of beta_hat_t = A v_{t+1}: this wave's v is its own k-blocks' B operand
+            accn = f64x4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int r = 0; r < 4; ++r) accn = mfma_f64(aop[r], v[r], accn);
         };
         // consume(t): after the barrier, beta_hat_t = A v_{t+1} (:163-199, this wave's 16 rows), gamma_t,
         // then the xi MFMAs of the same image.  The xi products are off the beta chain: they are made
@@ -337,15 +366,15 @@ __global__ void __launch_bounds__(NT * 64, 2) k_estep_mfma(EArgs a) {  // 2 wave
             const bool reg = !MASK || t <= T - 2;
             const int p = t & 1;
             if (!WIDE_ABL(a, 16)) __syncthreads();
-            const double *vsrc = bopb + p * IMG;
-            f64x4 acc = {0.0, 0.0, 0.0, 0.0};
+            const double *vsrc = bopr + p * IMGX;
+            f64x4 acc = accn;  // own blocks done (publish), the other waves' blocks now
 #pragma unroll
-            for (int kb = 0; kb < KB; ++kb) acc = mfma_f64(aop[kb], vsrc[4 * kb * kXs], acc);
+            for (int kb = 4; kb < KB; ++kb) acc = mfma_f64(aop[kb], vsrc[4 * kb * kXs], acc);
             // S_ij += sum_s z_t(i, s) v_{t+1}(j, s): xi_t(i,j) / a_ij (:396-410)
-            const double *tsrc = topb + p * IMG;
+            const double *tsrc = topb + p * IMGX;
             double za[4];
 #pragma unroll
-            for (int kk = 0; kk < 4; ++kk) za[kk] = tsrc[2 * IMG + 16 * m * kXs + 4 * kk];
+            for (int kk = 0; kk < 4; ++kk) za[kk] = topz[p * IMG + 16 * m * kXs + 4 * kk];
             asm volatile("" : "+v"(za[0]) : "v"(acc[0]));  // xi after the beta chain (see above)
             f64x4 gm;
 #pragma unroll

@@ -746,10 +746,10 @@ int plan_estep(hmmbw_ctx *c, bool fwd_only, const IterState *state, double *copi
     const int wpb = kBlock / kWave;
     p.grid = (unsigned)c->nblocks;
     if (c->wide) {
-        // [2 or 4][NP][17] exchange images + per-block reduction scratch (estep_mfma.hpp)
+        // exchange images [2][2 NP][17] (+ the backward's masked-z images [2][NP][17]) and the per-block
+        // reduction scratch (estep_mfma.hpp)
         const int nt = c->NP / 16;
-        p.lds = sizeof(double) * ((fwd_only ? 2 * (size_t)c->NP * 17 : 4 * (size_t)c->NP * 17 + (size_t)nt * 4 * nt * 64) +
-                                  (size_t)nt * 16 + 16);
+        p.lds = sizeof(double) * ((fwd_only ? 4 * (size_t)c->NP * 17 : 6 * (size_t)c->NP * 17) + (size_t)nt * 16 + 16);
         const Kernels kw = wide_kernels(c->NP);
         p.fn = fwd_only ? kw.score : (c->det ? kw.det_estep : kw.estep);
         p.block = (unsigned)(nt * kWave);

@@ -62,10 +62,6 @@ static __device__ unsigned long long g_chunk[4096][2][64];
     } while (0)
 #endif
 
-#ifndef HMMBW_HIST_SPLIT  // A/B only: 0 puts every slot's histogram adds into the first half of the H entries
-#define HMMBW_HIST_SPLIT 1
-#endif
-
 constexpr int kWave = 64;
 constexpr int kChunk = 8;  // time steps per packed symbol load (8 x uint16 = 16 B)
 #ifndef HMMBW_KSCALE
@@ -403,23 +399,20 @@ __host__ __device__ constexpr bool lds_tables_fit(int K, int GP) { return (size_
 __host__ __device__ constexpr size_t lds_table_bytes(int K, int GP) { return (size_t)kHistOff + (size_t)K * GP * 16; }
 
 // Entry i = k * GP + c (symbol k, state column c) of the LDS emission tables, 16 B each:
-// P {a_cc b_c(k), a_{c-1,c} b_c(k)} (left-to-right, PT) or {b_c(k), 0} (dense); H {h, h'}: two histogram
-// accumulators, the wave's even sequence slots adding into h and the odd ones into h' (summed at the flush).
-// A ds_add_f64 serves 16 contiguous lanes per LDS cycle, i.e. two sequence slots x 8 states, and banks
-// repeat every 128 B: with one accumulator per 16-B entry both slots' 8 lanes hit the same 8 even banks
-// of their rows (a 2-way conflict on every step); with the slot's own half they are conflict-free.
-// (Round 4 also measured a dense layout with two 8-B copies of b per row, one per sequence-slot parity, to
-// spread the ds_read_b64 lane groups over more banks: 74.0-76.7 us at cfg3 against 73.4, no gain.)
+// P {a_cc b_c(k), a_{c-1,c} b_c(k)} (left-to-right, PT) or {b_c(k), 0} (dense); H {histogram, b_c(k)}.
+// Round 4 measured two alternatives, both reverted: a dense layout with two 8-B copies of b per row (one
+// per sequence-slot parity, to spread the ds_read_b64 lane groups over more banks: 74.0-76.7 us at cfg3
+// against 73.4), and H entries {h, h'} with the even / odd sequence slots adding into their own half (a
+// ds_add_f64 serves 16 contiguous lanes = two slots x 8 states, and both slots' adds otherwise hit the same
+// 8 even banks), b(o_0) then coming from the statistics: LR cfg3 36.96-36.98 us against 35.23-35.58.
 template <bool PT, int GP>
 __device__ __forceinline__ void tab_put(double *sP, double *sH, int i, double px, double py, double b) {
     reinterpret_cast<double2 *>(sP)[i] = PT ? double2{px, py} : double2{b, 0.0};
-    reinterpret_cast<double2 *>(sH)[i] = double2{0.0, 0.0};
+    reinterpret_cast<double2 *>(sH)[i] = double2{0.0, b};
 }
 
 template <int N, int G, int GP, bool PT, int BLK = kBlock>
 __device__ bool merged_mstep(const EArgs &a, double *sP, double *sH, double *sPA, long long bid);
-__device__ __forceinline__ double mstep_inv(double den);
-__device__ __forceinline__ double bnum_to_b(double num, double inv);
 __device__ int rank_ll_count(const EArgs &a);
 __device__ void rank_ll_fold(const EArgs &a, long long nblk);
 
@@ -448,7 +441,7 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
     // left-to-right with LDS tables: per (symbol, state) products {a_jj b_j(o), a_{j-1,j} b_j(o)}
     constexpr bool PT = LR && LDSTAB;
     extern __shared__ __attribute__((aligned(256))) double smem[];  // 256-B aligned whatever the static LDS (ds_read_b128 rows)
-    __shared__ double sPA[2 * G + N * N];  // pi (zero-padded to G), A and 1 / gamma_den_all of this iteration
+    __shared__ double sPA[G + N * N];  // pi (zero-padded to G) and A of this iteration
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     PHASE(0);
     if constexpr (!FWD_ONLY)  // clear the next iteration's statistics (single rank: triple buffer)
@@ -466,19 +459,6 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
     const bool xblk = bid >= a.nfull;
     const long long wave = xblk ? a.nfull * wpb + (bid - a.nfull) * a.xact + wv : bid * wpb + wv;
     const bool wactive = !xblk || wv < a.xact;
-    // PT, merged: b_j(o_0) is the merged M-step's bnum_to_b of the summed statistics (the H entries hold
-    // histograms only); its three dependent loads (wave layout, first pack, statistics) start here, ahead
-    // of the prologue, whose ~5 us they overlap
-    double b0num = 0.0;
-    if constexpr (PT && !FWD_ONLY) {
-        if (merged && wactive && wave < a.L.nwaves) {
-            const uint4 p0 = *reinterpret_cast<const uint4 *>(a.L.sym + a.L.wave_symoff[wave] + u * kChunk);
-            const long long idx = a.m.off_bnum + (long long)((unsigned)sym_of(p0, 0) / (unsigned)(GP * 16)) * N +
-                                  (j < N ? j : 0);
-            b0num = a.m.src[idx];
-            for (int c = 1; c < a.m.nsrc; ++c) b0num += a.m.src[c * a.m.copy_len + idx];
-        }
-    }
     if (merged) {
         // the previous iteration's M-step, computed redundantly by every workgroup straight into
         // its LDS tables (no separate M-step kernel, no parameter round trip through HBM)
@@ -488,7 +468,6 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
         if (a.state != nullptr && a.state->done) return;  // converged: device-side no-op
         if (tid < G) sPA[tid] = tid < N ? a.pi[tid] : 0.0;
         if (tid < N * N) sPA[G + tid] = a.A[tid];
-        if (tid < G) sPA[G + N * N + tid] = 0.0;  // unused: b(o_0) comes from B^T when not merged
         if constexpr (LDSTAB) {
             if constexpr (PT) __syncthreads();  // the records fold a_jj, a_{j-1,j} in
             // 16 independent loads in flight per thread before the first LDS store
@@ -641,17 +620,8 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
 #pragma unroll
             for (int i = 0; i < 4; ++i) Q[i] = loadpack(i < nch ? i : nch - 1);
             double b00;  // b_j(o_0) for pi_j b_j(o_0) (:357-360)
-            if constexpr (PT) {
-                // b_j(o_0), exactly as the table's entry was formed: the merged M-step's bnum_to_b of the summed
-                // statistics, or B^T (from which the table was built)
-                if (merged) {
-                    b00 = jv ? bnum_to_b(b0num, sPA[G + N * N + j]) : 0.0;
-                } else {
-                    b00 = a.Bt[(size_t)((unsigned)sym_of(Q[0], 0) / (unsigned)(GP * 16)) * G + j];
-                }
-            } else {
-                b00 = *brow(Q[0], 0);
-            }
+            if constexpr (PT) b00 = *reinterpret_cast<const double *>(pent(Q[0], 0) + kHistOff + 8);  // H.b
+            else b00 = *brow(Q[0], 0);
             Em E[2][kChunk];
 #pragma unroll
             for (int k = 0; k < kChunk; ++k) E[0][k] = ld_em(Q[0], k);
@@ -817,7 +787,6 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
                 // chunk's emission rows are read (one chunk ahead) and reused by its histogram atomics
                 // (32-bit LDS byte addresses, the table base included, so the atomics need no add)
                 unsigned HA[2][kChunk];
-                const unsigned hodd = HMMBW_HIST_SPLIT ? (unsigned)(u & 1) * 8u : 0u;  // this slot's half of the H entries
                 auto ldrows = [&](Em (&bv)[kChunk], double (&bu)[kChunk], unsigned (&ha)[kChunk], const uint4 &p) {
 #pragma unroll
                     for (int k = 0; k < kChunk; ++k) {
@@ -959,7 +928,7 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
                         // columns), so the compiler's lgkmcnt bookkeeping stays exact
 #pragma unroll
                         for (int k = 0; k < kChunk; ++k)  // :474-485
-                            atomicAdd(reinterpret_cast<double *>(lds_ptr(hac[k] + hodd) + kHistOff), gk[k]);  // H.h / H.h' of o_t
+                            atomicAdd(reinterpret_cast<double *>(lds_ptr(hac[k]) + kHistOff), gk[k]);  // H.h of o_t
                     } else if (N == G || jv) {
 #pragma unroll
                         for (int k = 0; k < kChunk; ++k)
@@ -1059,7 +1028,7 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
         for (int idx = tid; idx < K * G; idx += blockDim.x) {
             const int k = idx / G, jj = idx - k * G;
             if (jj >= N) continue;
-            const double x = sH[((size_t)k * GP + jj) * 2] + sH[((size_t)k * GP + jj) * 2 + 1];
+            const double x = sH[((size_t)k * GP + jj) * 2];
             if (x != 0.0) unsafeAtomicAdd(&accb[a.off_bnum + (long long)k * N + jj], x);
         }
     }
@@ -1664,7 +1633,6 @@ __device__ bool merged_mstep(const EArgs &a, double *sP, double *sH, double *sPA
     PHASE(7);
     // pi (:415-424), A (:429-455) into LDS
     if (tid < G) sPA[tid] = (tid < N && sSm[tid] > 0.0) ? sSm[tid] / (double)m.R_global : 0.0;
-    if (tid < G) sPA[G + N * N + tid] = tid < N ? mstep_inv(sSm[N + N * N + N + tid]) : 0.0;  // b(o_0), estep_small_body
     if (tid < N * N) {
         const double den = sSm[N + N * N + tid / N];
         const double num = sSm[N + tid];
