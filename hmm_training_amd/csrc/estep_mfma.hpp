@@ -119,13 +119,19 @@ __global__ void __launch_bounds__(NT * 64, 2) k_estep_mfma(EArgs a) {  // 2 wave
         const double2 lo = p[0], hi = p[1];
         return f64x4{lo.x, lo.y, hi.x, hi.y};
     };
-    // Own block first.  The recursions contract over all NP states in k-blocks of 4, and the C/D registers
-    // of this wave's block ARE the B operands of its own 4 k-blocks (4m + r: states 16m + 4r + g), so each
-    // step issues those 4 MFMAs straight from registers BEFORE the barrier and the LDS reads of the other
-    // waves' blocks, which the wave reads in the rotated order 16m + 16, ..., 16m + NP - 1 (mod NP, hence
-    // the doubled image rows); the A operands are loaded in the same rotated k-block order.  That hides
-    // part of the exchange (LDS write, barrier, LDS read) behind matrix work.
-    double *const putb = X0 + (16 * m + g) * kXs + s;   // this wave's block, both copies
+    // Backward: own block first.  The recursion contracts over all NP states in k-blocks of 4, and the C/D
+    // registers of this wave's block ARE the B operands of its own 4 k-blocks (4m + r: states 16m + 4r + g),
+    // so publish issues those 4 MFMAs of the next step's beta straight from registers, before the barrier
+    // and the LDS reads of the other waves' blocks, which consume then reads in the rotated order 16m + 16,
+    // ..., 16m + NP - 1 (mod NP, hence the doubled v-image rows), with the A operands loaded in the same
+    // rotated k-block order (backward 3,210 -> 3,096 cycles per step for a lone tile).  The forward keeps
+    // the natural order and one copy: the same reordering there cost 46 cycles per step (its extra LDS
+    // writes sit in front of the barrier and its exchange has no independent MFMAs to hide behind).
+    double *const putb = X0 + (16 * m + g) * kXs + s;   // this wave's block (put2: both copies)
+    auto put1 = [&](int p, const f64x4 &v) HMMBW_AI {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) putb[p * IMGX + 4 * r * kXs] = v[r];
+    };
     auto put2 = [&](int p, const f64x4 &v) HMMBW_AI {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -138,6 +144,7 @@ __global__ void __launch_bounds__(NT * 64, 2) k_estep_mfma(EArgs a) {  // 2 wave
 #pragma unroll
         for (int r = 0; r < 4; ++r) putz[p * IMG + 4 * r * kXs] = v[r];
     };
+    const double *const bopb = X0 + g * kXs + s;             // + 4 kb kXs: k-block kb of image p (forward)
     const double *const bopr = X0 + (16 * m + g) * kXs + s;  // + 4 kb' kXs: rotated k-block kb' (>= 4) of image p
     const double *const topb = X0 + (lane & 15) * kXs + (lane >> 4);
     const double *const topz = Z0 + (lane & 15) * kXs + (lane >> 4);
@@ -151,10 +158,10 @@ __global__ void __launch_bounds__(NT * 64, 2) k_estep_mfma(EArgs a) {  // 2 wave
 
     // forward A operands of this wave's 16-state block: A^T[o][i] = a_io (o = 16m + (lane&15),
     // i = 4kb + (lane>>4))
-    double aop[KB];  // rotated k-block order: aop[kb'] is k-block (kb' + 4m) mod KB
+    double aop[KB];
 #pragma unroll
     for (int kb = 0; kb < KB; ++kb) {
-        const int o = 16 * m + (lane & 15), i = 4 * ((kb + 4 * m) % KB) + (lane >> 4);
+        const int o = 16 * m + (lane & 15), i = 4 * kb + (lane >> 4);
         aop[kb] = (i < N && o < N) ? a.A[i * N + o] : 0.0;
     }
 
@@ -179,36 +186,27 @@ __global__ void __launch_bounds__(NT * 64, 2) k_estep_mfma(EArgs a) {  // 2 wave
                 x[r] = (j < N && T > 0) ? a.pi[j] * b[r] : 0.0;  // pi_j b_j(o_0) (:357-360)
             }
         } else {
-            // one accumulation chain: a dependent v_mfma_f64_16x16x4 issues every 64 cycles, its full
-            // rate (tools/ubench_mfma.hip), and a second chain would cost 8 VGPRs.  Own block first, from
-            // the registers (z = z_{t-1}), then the barrier after which the other waves' z_{t-1} is readable
-            f64x4 acc = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-            for (int r = 0; r < 4; ++r) acc = mfma_f64(aop[r], z[r], acc);
-            // keep the own-block MFMAs in front of the barrier (they touch no memory, so the scheduler would
-            // move them behind it, and the LDS reads behind them)
-            __builtin_amdgcn_sched_barrier(0);
-            if (!WIDE_ABL(a, 16)) __syncthreads();
-            const double *src = bopr + ((t - 1) & 1) * IMGX;
+            const double *src = bopb + ((t - 1) & 1) * IMGX;
             double zb[KB];
 #pragma unroll
-            for (int kb = 4; kb < KB; ++kb) zb[kb] = src[4 * kb * kXs];
+            for (int kb = 0; kb < KB; ++kb) zb[kb] = src[4 * kb * kXs];
+            // one accumulation chain: a dependent v_mfma_f64_16x16x4 issues every 64 cycles, its full
+            // rate (tools/ubench_mfma.hip), and a second chain would cost 8 VGPRs
+            f64x4 acc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-            for (int kb = 4; kb < KB; ++kb) acc = mfma_f64(aop[kb], zb[kb], acc);
+            for (int kb = 0; kb < KB; ++kb) acc = mfma_f64(aop[kb], zb[kb], acc);
             // s_t from z_{t-1} over all NP states of the sequence (4 lanes x KB values)
             int M = 0;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) M = max(M, bexp(z[r]));
-#pragma unroll
-            for (int kb = 4; kb < KB; ++kb) M = max(M, bexp(zb[kb]));
+            for (int kb = 0; kb < KB; ++kb) M = max(M, bexp(zb[kb]));
             // across the 4 lane rows: gfx950's row-swap permutes are VALU ops (ds_bpermute put two LDS
             // round trips in front of the MFMA chain, which the compiler schedules after them)
             M = row_max4(M);
             // the exponent's VALU work between the chain's MFMAs (each waits ~64 cycles for the last)
             // instead of in front of the first one
-            __builtin_amdgcn_sched_group_barrier(0x100, (KB - 4) / 2, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, KB / 2, 0);
 #pragma unroll
-            for (int kb = 4; kb < KB; ++kb) {
+            for (int kb = 0; kb < KB; ++kb) {
                 __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
                 __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
             }
@@ -226,7 +224,7 @@ __global__ void __launch_bounds__(NT * 64, 2) k_estep_mfma(EArgs a) {  // 2 wave
             z = x;
         }
         C += sc;
-        put2(t & 1, z);
+        put1(t & 1, z);
         if constexpr (!FWD_ONLY) {
             if (!WIDE_ABL(a, 8)) {
 #pragma unroll
@@ -236,7 +234,7 @@ __global__ void __launch_bounds__(NT * 64, 2) k_estep_mfma(EArgs a) {  // 2 wave
             // lanes, the same value to the same 16 words, so the store needs no exec branch)
             if (STEADY || (m == 0 && g == 0)) ew[t * kTileSeqs] = sc;
         }
-        // no barrier here: the next step issues its own-block MFMAs first (above)
+        if (!WIDE_ABL(a, 16)) __syncthreads();
     };
     uint4 p0, p1;  // symbol packs of chunks c and c + 1
     auto fchunk = [&](int c, auto MASK_, auto STEADY_) HMMBW_AI {
