@@ -13,10 +13,11 @@ then one statistics pass (hmmbw_estep) with the final parameters against oracle.
     and the sum rules (sum_k B_num = gamma_den_all, sum_j xi = gamma_den_excl, sum pi_num = R,
     sum gamma_den_all = R T).
 Configurations: cfg3 (10,000 x 200, N=8, K=256) left-to-right and dense, the cfg4 per-GPU shard
-(12,500 x 200) on skewed 'H' symbols, cfg4 whole (100,000 x 200) on one GPU (one iteration), a
-full-shape cfg5 slice (512 x 400, N=64, K=1024, dense) and the cfg5 per-GPU shard (6,250 x 400) against
-the oracle, and the whole cfg5 set (50,000 x 400) on one GPU by sum rules and 64 sampled log P (the
-oracle would need minutes per iteration there).
+(12,500 x 200) on skewed 'H' symbols, cfg4 whole (100,000 x 200) on one GPU (two iterations), a
+full-shape cfg5 slice (512 x 400, N=64, K=1024, dense), the cfg5 per-GPU shard (6,250 x 400), and the
+whole cfg5 set (50,000 x 400) on one GPU as four ranks through the split ABI: each quarter's complete
+statistics against the oracle on that quarter, and the iteration (L, M-step) against the merged oracle
+quarters.
 """
 import ctypes
 import sys
