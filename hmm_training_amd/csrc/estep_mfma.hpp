@@ -38,6 +38,15 @@ namespace hmmbw {
 typedef double f64x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kTileSeqs = 16;  // sequences per tile = MFMA columns
+// The gamma rows (1.28 GB per cfg5-shard iteration, written once by the E-step, read once by the gather)
+// move with nontemporal stores and loads: E-step + gather 1,714 -> 1,672 us (the gather 233 -> 193 us).
+#ifndef HMMBW_GAMMA_NT
+#define HMMBW_GAMMA_NT 1
+#endif
+// alpha_hat (written by the forward, read once by the backward) likewise: E-step 1,480-1,488 -> 1,476-1,481 us
+#ifndef HMMBW_ALPHA_NT
+#define HMMBW_ALPHA_NT 1
+#endif
 
 // Profiling ablations of the inner loops (results wrong by construction) exist only in a diagnostics
 // build (-DHMMBW_WIDE_ABLATE): a runtime test inside the step loops costs the release build its
@@ -107,8 +116,15 @@ __global__ void __launch_bounds__(NT * 64, 2) k_estep_mfma(EArgs a) {  // 2 wave
     const unsigned *gdw = a.gdst + (FWD_ONLY ? 0 : a.L.wave_ckoff[tile] / NP) + s;
     auto putg = [&](unsigned row, const f64x4 &v) HMMBW_AI {
         double2 *q = reinterpret_cast<double2 *>(a.gam + (long long)row * NP + col0);
-        q[0] = double2{v[0], v[1]};
-        q[1] = double2{v[2], v[3]};
+        if constexpr (HMMBW_GAMMA_NT) {  // written once here, read once by the gather
+            typedef double d2 __attribute__((ext_vector_type(2)));
+            d2 *qq = reinterpret_cast<d2 *>(q);
+            __builtin_nontemporal_store(d2{v[0], v[1]}, qq);
+            __builtin_nontemporal_store(d2{v[2], v[3]}, qq + 1);
+        } else {
+            q[0] = double2{v[0], v[1]};
+            q[1] = double2{v[2], v[3]};
+        }
     };
 
     auto loadpack = [&](int c) HMMBW_AI -> uint4 {
@@ -228,7 +244,10 @@ __global__ void __launch_bounds__(NT * 64, 2) k_estep_mfma(EArgs a) {  // 2 wave
         if constexpr (!FWD_ONLY) {
             if (!WIDE_ABL(a, 8)) {
 #pragma unroll
-                for (int r = 0; r < 4; ++r) ckw[((long long)t * NT * 4 + r) * 64] = z[r];
+                for (int r = 0; r < 4; ++r) {
+                    if constexpr (HMMBW_ALPHA_NT) __builtin_nontemporal_store(z[r], &ckw[((long long)t * NT * 4 + r) * 64]);
+                    else ckw[((long long)t * NT * 4 + r) * 64] = z[r];
+                }
             }
             // every wave computes the same s_t from all NP states: one lane group stores it (STEADY: all
             // lanes, the same value to the same 16 words, so the store needs no exec branch)
@@ -327,7 +346,10 @@ __global__ void __launch_bounds__(NT * 64, 2) k_estep_mfma(EArgs a) {  // 2 wave
             f64x4 v;
             if (WIDE_ABL(a, 8)) return f64x4{0.5, 0.5, 0.5, 0.5};
 #pragma unroll
-            for (int r = 0; r < 4; ++r) v[r] = ckw[((long long)t * NT * 4 + r) * 64];
+            for (int r = 0; r < 4; ++r) {
+                if constexpr (HMMBW_ALPHA_NT) v[r] = __builtin_nontemporal_load(&ckw[((long long)t * NT * 4 + r) * 64]);
+                else v[r] = ckw[((long long)t * NT * 4 + r) * 64];
+            }
             return v;
         };
         // publish(t): the image of step t <= Tw - 2 (MASK: per-sequence t <= T - 2 in ragged tiles) into
@@ -529,7 +551,8 @@ __global__ void __launch_bounds__(256) k_bnum_gather(const double *gam, const un
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const long long r = SORTED ? (pw + g + u < e ? pw + g + u : b) : (long long)__builtin_amdgcn_readlane(cur, g + u);
-                x[u] = gam[r * NP + q];
+                if constexpr (HMMBW_GAMMA_NT) x[u] = __builtin_nontemporal_load(&gam[r * NP + q]);
+                else x[u] = gam[r * NP + q];
             }
 #pragma unroll
             for (int u = 0; u < U; ++u) acc += (pw + g + u < e) ? x[u] : 0.0;

@@ -62,6 +62,12 @@ static __device__ unsigned long long g_chunk[4096][2][64];
     } while (0)
 #endif
 
+// 1: the dense path's stored z_t (written once, read once) nontemporal.  Measured worse (cfg3 dense 79.7-80.5
+// against 73.6-73.8 us): the backward reads them back while the caches still hold them.
+#ifndef HMMBW_ZF_NT
+#define HMMBW_ZF_NT 0
+#endif
+
 constexpr int kWave = 64;
 constexpr int kChunk = 8;  // time steps per packed symbol load (8 x uint16 = 16 B)
 #ifndef HMMBW_KSCALE
@@ -664,8 +670,12 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
                     }
                     sp[k] = st;
                     if constexpr (!FWD_ONLY) {
-                        if (ZF) ckw[((long long)c * kChunk + k) * kWave] = z;  // every z_t
-                        else if (k == 0) ckw[(long long)c * kWave] = z;    // checkpoint z_{8c}
+                        if (ZF) {  // every z_t
+                            if constexpr (HMMBW_ZF_NT) __builtin_nontemporal_store(z, &ckw[((long long)c * kChunk + k) * kWave]);
+                            else ckw[((long long)c * kChunk + k) * kWave] = z;
+                        } else if (k == 0) {
+                            ckw[(long long)c * kWave] = z;  // checkpoint z_{8c}
+                        }
                     }
                 }
                 if constexpr (!FWD_ONLY) spw[(long long)c * U] = pack_exps(sp);
@@ -771,7 +781,10 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
                 auto ldz = [&](double (&zz)[ZF ? kChunk : 1], int c) {
                     if constexpr (ZF) {
 #pragma unroll
-                        for (int k = 0; k < kChunk; ++k) zz[k] = ckw[((long long)c * kChunk + k) * kWave];
+                        for (int k = 0; k < kChunk; ++k) {
+                            if constexpr (HMMBW_ZF_NT) zz[k] = __builtin_nontemporal_load(&ckw[((long long)c * kChunk + k) * kWave]);
+                            else zz[k] = ckw[((long long)c * kChunk + k) * kWave];
+                        }
                     }
                 };
                 Ld X[4];
