@@ -442,8 +442,9 @@ def main(argv=None):
     offsets = np.arange(R + 1, dtype=np.int64) * T
     pi, A, B = init_params(N, K, topo, np.random.default_rng(seed))
 
+    # peer waits give up after 5 s (ranks enter each leg together after a barrier; a failed leg is dropped)
     eng = BaumWelchEngine(N, K, device=device, topology=topo, rank=rank, world_size=world,
-                          deterministic=args.deterministic, allreduce=args.allreduce)
+                          deterministic=args.deterministic, allreduce=args.allreduce, peer_timeout_ms=5000)
     t_up = time.perf_counter()
     eng.set_observations(offsets=offsets, symbols=symbols, n_seq_global=R * world)
     eng.set_params(pi, A, B)
@@ -482,9 +483,14 @@ def main(argv=None):
         elapsed = time.perf_counter() - t0
         r = {"gpu_ms_step": ev0.elapsed_time(ev1) / steps, "kern_ms": 0.0, "kern_n": 0, "est_ms": 0.0, "est_n": 0,
              "ar_ms": 0.0, "ar_n": 0}
-        st, _ = eng.status()
-        if st.iterations != n_iter[0]:
-            raise RuntimeError(f"expected {n_iter[0]} iterations, engine ran {st.iterations}")
+        # a device-side failure (a peer all-reduce timeout) is recorded, not raised, until every rank has
+        # passed the collective below: no rank may leave the leg while the others wait in it
+        try:
+            st, _ = eng.status()
+            r["error"] = None if st.iterations == n_iter[0] else \
+                f"expected {n_iter[0]} iterations, engine ran {st.iterations}"
+        except Exception as e:  # noqa: BLE001 - reported in the JSON line, or raised for the first leg
+            r["error"] = str(e)
         if world > 1:
             t = torch.tensor([elapsed], dtype=torch.float64,
                              device=f"cuda:{device}" if args.dist_backend == "nccl" else "cpu")
@@ -495,6 +501,15 @@ def main(argv=None):
         # E-step launches timed one by one (event pairs around each launch serialise the queue, so this
         # reads ~1-2 us above the undisturbed kernel), in a separate batch after the timed region; plus the
         # all-reduce per iteration on the engine's own path
+        if world > 1:  # every rank learns whether any rank failed
+            ok = torch.tensor([0 if r["error"] else 1], dtype=torch.int32,
+                              device=f"cuda:{device}" if args.dist_backend == "nccl" else "cpu")
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+            if int(ok.item()) == 0 and not r["error"]:
+                r["error"] = "another rank failed this leg"
+        if r["error"]:
+            r["allreduce"] = eng.allreduce
+            return r
         if not args.no_kernel_timing:
             eng.timing(1)
             eng.comm_info(reset=True)
@@ -506,14 +521,24 @@ def main(argv=None):
         r["allreduce"] = eng.allreduce
         return r
 
-    legs = {}
+    legs, failed = {}, {}
     first = leg(args.steps, args.warmup)
+    if first["error"]:
+        raise RuntimeError(first["error"])
     legs[first["allreduce"] or "none"] = first
     if world > 1 and args.allreduce == "both" and eng._rccl_ok and eng._peer_ok:
         # the other all-reduce on the same engine and data, same protocol: both are measured side by side
         other = "peer" if first["allreduce"] == "rccl" else "rccl"
         eng.set_allreduce(other)
-        legs[other] = leg(args.steps, max(2, min(args.warmup, 10)))
+        r2 = leg(args.steps, max(2, min(args.warmup, 10)))
+        if r2["error"]:
+            # the line still reports the first leg; the engine restarts from a clean state on it
+            failed[other] = r2["error"]
+            eng.set_allreduce(first["allreduce"])
+            eng.reset(0.0, 1 << 40)
+            n_iter[0] = 0
+        else:
+            legs[other] = r2
     # the headline is the faster leg (both run the full EM iteration; config.allreduce names it)
     best = max(legs, key=lambda k: -legs[k]["elapsed"])
     L = legs[best]
@@ -605,7 +630,8 @@ def main(argv=None):
                                   "ms_per_step": 1000.0 * v["elapsed"] / args.steps,
                                   "allreduce_us_per_iter": 1000.0 * v["ar_ms"] / v["ar_n"] if v["ar_n"] else None,
                                   "kernel_ms_per_launch_events": v["kern_ms"] / v["kern_n"] if v["kern_n"] else None}
-                              for k, v in legs.items()}}
+                              for k, v in legs.items()},
+                     "legs_failed": failed}
             if world > 1 else None,
             "synced": synced,
             "upload_s": upload_s,
