@@ -81,9 +81,17 @@ __device__ __forceinline__ f64x4 mfma_f64(double a, double b, f64x4 c) {
 // prefix [0, off_bnum) is owned by exactly one lane, accumulated in registers in a fixed order and
 // stored once into the workgroup's partial a.part[block][off_bnum] (k_det_reduce sums the partials in
 // workgroup order; the B numerator is the gather's, deterministic already).
-template <int NT, bool FWD_ONLY, bool DET = false>
+// WQ (work queue): 2 ntile workgroups, each taking the next work unit from a counter as it starts:
+// units [0, ntile) are the tiles' forward sweeps, [ntile, 2 ntile) their backward sweeps, each backward
+// waiting for its tile's forward (a per-tile flag; alpha_hat and s_t pass through HBM, released at agent
+// scope).  The dispatcher starts a workgroup wherever one finished, so with more tiles than CUs the CUs'
+// loads even out in units of a sweep instead of a whole tile (cfg5 shard: 391 tiles on 256 CUs left 135
+// CUs two tiles and the others one).  A unit only waits for a unit taken before it, by a workgroup that
+// is running, so the waits always end.
+template <int NT, bool FWD_ONLY, bool DET = false, bool WQ = false>
 __global__ void __launch_bounds__(NT * 64, 2) k_estep_mfma(EArgs a) {  // 2 waves per SIMD: <= 256 VGPRs
     static_assert(!(DET && FWD_ONLY), "deterministic mode is an E-step option");
+    static_assert(!WQ || (!DET && !FWD_ONLY), "the work queue is an E-step option (atomic statistics)");
     constexpr int NP = 16 * NT, KB = 4 * NT, IMG = NP * kXs, IMGX = 2 * IMG;
     extern __shared__ __attribute__((aligned(256))) double smem[];  // 256-B aligned whatever the static LDS (ds_read_b128 rows)
     // [2][2 NP][kXs]: z (forward) / v (backward) images, every row stored twice (rows r and r + NP), so that
@@ -100,7 +108,19 @@ __global__ void __launch_bounds__(NT * 64, 2) k_estep_mfma(EArgs a) {  // 2 wave
     const int tid = threadIdx.x, lane = tid & 63, m = tid >> 6;
     const int s = lane & 15, g = lane >> 4;
     const int N = a.N;
-    const long long tile = blockIdx.x;
+    const long long ntile = WQ ? (long long)a.wq_units : (long long)gridDim.x;
+    bool do_f = true;  // this workgroup runs the tile's forward sweep ...
+    bool do_b = true;  // ... and its backward sweep
+    long long tile = blockIdx.x;
+    if constexpr (WQ) {
+        __shared__ int s_unit;
+        if (tid == 0) s_unit = (int)atomicAdd(a.wq, 1u);
+        __syncthreads();
+        const long long u = s_unit;
+        do_f = u < ntile;
+        do_b = !do_f;
+        tile = do_f ? u : u - ntile;
+    }
     const long long slot = tile * kTileSeqs + s;
     const int T = a.L.slot_len[slot];
     const int seq = a.L.slot_seq[slot];
@@ -175,10 +195,12 @@ __global__ void __launch_bounds__(NT * 64, 2) k_estep_mfma(EArgs a) {  // 2 wave
     // forward A operands of this wave's 16-state block: A^T[o][i] = a_io (o = 16m + (lane&15),
     // i = 4kb + (lane>>4))
     double aop[KB];
+    if (do_f) {
 #pragma unroll
-    for (int kb = 0; kb < KB; ++kb) {
-        const int o = 16 * m + (lane & 15), i = 4 * kb + (lane >> 4);
-        aop[kb] = (i < N && o < N) ? a.A[i * N + o] : 0.0;
+        for (int kb = 0; kb < KB; ++kb) {
+            const int o = 16 * m + (lane & 15), i = 4 * kb + (lane >> 4);
+            aop[kb] = (i < N && o < N) ? a.A[i * N + o] : 0.0;
+        }
     }
 
     // ---------------- forward (hmm_training.py:357-368; hmm_testing.py:70-92) ----------------
@@ -281,8 +303,30 @@ __global__ void __launch_bounds__(NT * 64, 2) k_estep_mfma(EArgs a) {  // 2 wave
         for (int c = 1; c < cf; ++c) fchunk(c, MASK_, std::true_type{});
         for (int c = cf > 1 ? cf : 1; c < nch; ++c) fchunk(c, MASK_, std::false_type{});
     };
-    if (full) forward(std::false_type{});
-    else forward(std::true_type{});
+    if (do_f) {
+        if (full) forward(std::false_type{});
+        else forward(std::true_type{});
+    } else if constexpr (WQ) {
+        // backward unit: wait for the tile's forward (bounded: it runs on a resident workgroup), then
+        // z_{Tw-1} (masked per sequence, as the forward left it in its registers) from alpha_hat
+        if (tid == 0) {
+            const unsigned long long t0 = wall_clock64();
+            while (__hip_atomic_load(a.wq_flag + tile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
+                if (wall_clock64() - t0 > 1000000000ull) break;  // 10 s: never hang the device
+                __builtin_amdgcn_s_sleep(8);
+            }
+        }
+        __syncthreads();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        if (Tw > 0) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const double *q = &ckw[((long long)(Tw - 1) * NT * 4 + r) * 64];
+                if constexpr (HMMBW_ALPHA_NT) z[r] = __builtin_nontemporal_load(q);
+                else z[r] = *q;
+            }
+        }
+    }
 
     CHUNKSTAMP(0, 61);
     // log P(O|lambda) = log(sum_j z_{T-1}(j)) + ln2 * C   (:375-377)
@@ -296,10 +340,10 @@ __global__ void __launch_bounds__(NT * 64, 2) k_estep_mfma(EArgs a) {  // 2 wave
     for (int mm = 0; mm < NT; ++mm) phat += sRed[mm * kTileSeqs + s];
     const bool alive = (T > 0) && (phat > 0.0);
     const double lp = alive ? (log(phat) + (double)C * 0.69314718055994530942) : -INFINITY;
-    if (m == 0 && g == 0 && T > 0 && seq >= 0) a.logp[seq] = lp;
+    if (do_f && m == 0 && g == 0 && T > 0 && seq >= 0) a.logp[seq] = lp;
     const bool ll_valid = (m == 0) && (g == 0) && (T > 0);
 
-    if constexpr (!FWD_ONLY) if (!(a.ablate & 2)) {
+    if constexpr (!FWD_ONLY) if (do_b && !(a.ablate & 2)) {
         // ------------- backward fused with gamma / xi / M-step numerators (:370-410, :474-485) -------------
         double *accb = a.copies + (long long)(blockIdx.x % a.ncopies) * a.copy_len;
         double dgall[4] = {0.0, 0.0, 0.0, 0.0}, dpin[4] = {0.0, 0.0, 0.0, 0.0};  // DET: this lane's sums
@@ -499,6 +543,32 @@ __global__ void __launch_bounds__(NT * 64, 2) k_estep_mfma(EArgs a) {  // 2 wave
                 unsafeAtomicAdd(&accb[a.off_gall + j], x0);  // gamma_den_all = excl + the last frames
             }
         }
+    }
+    if constexpr (WQ) {
+        if (do_f) {  // the tile's log P pair, then the release of alpha_hat and s_t to its backward unit
+            __syncthreads();
+            block_ll_partial(lp, ll_valid, sRed + NT * kTileSeqs, a.llpart + 2 * tile);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            __syncthreads();
+            if (tid == 0) __hip_atomic_store(a.wq_flag + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else if (a.rank_ll != nullptr) {
+            __syncthreads();
+            int ticket = 0;
+            if (threadIdx.x == 0) ticket = rank_ll_count(a);
+            if ((threadIdx.x >> 6) == 0 && __shfl(ticket, 0) == (int)(ntile - 1)) rank_ll_fold(a, ntile);
+        }
+        // the last workgroup out re-arms the queue and the flags for the next launch
+        __shared__ int s_last;
+        if (tid == 0) s_last = atomicAdd(a.wq + 1, 1u) == gridDim.x - 1;
+        __syncthreads();
+        if (s_last) {
+            for (long long i = tid; i < ntile; i += blockDim.x) a.wq_flag[i] = 0u;
+            if (tid == 0) {
+                a.wq[0] = 0u;
+                a.wq[1] = 0u;
+            }
+        }
+        return;
     }
     __syncthreads();
     block_ll_partial(lp, ll_valid, sRed + NT * kTileSeqs, a.llpart + 2 * (long long)blockIdx.x);

@@ -13,6 +13,13 @@ Kernels wide_kernels(int NP) {
     return k;
 }
 
+KernelFn wide_wq_kernel(int NP) {
+    if (NP == 32) return k_estep_mfma<2, false, false, true>;
+    if (NP == 48) return k_estep_mfma<3, false, false, true>;
+    if (NP == 64) return k_estep_mfma<4, false, false, true>;
+    return nullptr;
+}
+
 BnumFn bnum_gather_kernel(bool sorted) { return sorted ? k_bnum_gather<true> : k_bnum_gather<false>; }
 
 }  // namespace hmmbw

@@ -482,6 +482,8 @@ struct hmmbw_ctx {
     double *d_gam = nullptr;
     long long *d_bptr = nullptr;
     unsigned *d_brows = nullptr;
+    unsigned *d_wq = nullptr;  // wide work queue (EArgs::wq): 2 counters + a flag per tile, or nullptr
+    long long wq_grid = 0;     // its grid (a workgroup per unit: 2 x tiles)
     uint4 *d_sp = nullptr;
     int *d_ebuf = nullptr;
     // native RCCL communicator (hmmbw_comm_init): the multi-rank hmmbw_iterate all-reduces d_ext
@@ -593,7 +595,8 @@ void free_obs(hmmbw_ctx *c) {
     dfree(c->d_sym); dfree(c->d_wsym); dfree(c->d_wckoff); dfree(c->d_wspoff);
     dfree(c->d_wT); dfree(c->d_wfull); dfree(c->d_slen); dfree(c->d_sseq);
     dfree(c->d_ck); dfree(c->d_sp); dfree(c->d_ebuf); dfree(c->d_logp); dfree(c->d_llpart); dfree(c->d_zf);
-    dfree(c->d_gam); dfree(c->d_bptr); dfree(c->d_brows); dfree(c->d_part);
+    dfree(c->d_gam); dfree(c->d_bptr); dfree(c->d_brows); dfree(c->d_part); dfree(c->d_wq);
+    c->wq_grid = 0;
     c->has_obs = false;
 }
 
@@ -754,6 +757,14 @@ int plan_estep(hmmbw_ctx *c, bool fwd_only, const IterState *state, double *copi
         p.fn = fwd_only ? kw.score : (c->det ? kw.det_estep : kw.estep);
         p.block = (unsigned)(nt * kWave);
         if (!p.fn) return fail(HMMBW_E_UNSUPPORTED, "no wide kernel for N");
+        if (!fwd_only && !c->det && c->d_wq) {  // more tiles than CUs: the work-queue form (estep_mfma.hpp)
+            p.fn = wide_wq_kernel(c->NP);
+            p.grid = (unsigned)c->wq_grid;
+            a.wq = c->d_wq;
+            a.wq_flag = c->d_wq + 2;
+            a.wq_units = (int)c->nblocks;
+            if (!p.fn) return fail(HMMBW_E_UNSUPPORTED, "no wide work-queue kernel for N");
+        }
     } else {
         const bool lr = c->topo == HMMBW_TOPOLOGY_LEFT_TO_RIGHT;
         const bool lds_tab = c->lds_tables();
@@ -1264,6 +1275,27 @@ int hmmbw_set_observations(hmmbw_ctx *c, const int64_t *offsets, const int32_t *
     }
     if (!rc) rc = dalloc(&c->d_logp, (size_t)std::max<int64_t>(R, 1));
     if (!rc) rc = dalloc(&c->d_llpart, 4 * (size_t)std::max(nblocks, 1LL));
+    // Wide path with many tiles per CU: a workgroup per forward and per backward sweep, taken from a queue
+    // in dispatch order (k_estep_mfma<..., WQ>), so the CUs' loads even out in sweeps instead of whole
+    // tiles.  Measured (round 4): whole cfg5 (3,125 tiles) 12.06 against 12.37 ms per iteration; the cfg5
+    // shard (391 tiles, 1.5 per CU) 2.17 against 1.85 ms: with so few tiles per CU the backward sweeps
+    // (0.63 of a tile) start late and form the tail, so the queue is used from 4 tiles per CU.
+    // HMMBW_WIDE_WQ=0 / 1 turns it off / on whenever there are more tiles than CUs.
+    long long wq_grid = 0;
+    if (!rc && c->wide && !c->det) {
+        int ncu = 0;
+        (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device);
+        const char *we = std::getenv("HMMBW_WIDE_WQ");
+        const long long from = (we && std::atoi(we) == 1) ? ncu : 4LL * ncu;
+        if (ncu > 0 && nblocks > from && !(we && std::atoi(we) == 0) && nblocks < (1LL << 30)) {
+            wq_grid = 2 * nblocks;
+            rc = dalloc(&c->d_wq, (size_t)nblocks + 2);
+            if (!rc) {
+                const hipError_t e = hipMemset(c->d_wq, 0, sizeof(unsigned) * ((size_t)nblocks + 2));
+                if (e != hipSuccess) return fail(HMMBW_E_HIP, std::string("hipMemset: ") + hipGetErrorString(e));
+            }
+        }
+    }
     if (rc) return rc;
     HIP_TRY(hipMemcpy(c->d_sym, hsym.data(), sizeof(uint16_t) * hsym.size(), hipMemcpyHostToDevice));
     if (c->wide || c->det) {
@@ -1288,6 +1320,7 @@ int hmmbw_set_observations(hmmbw_ctx *c, const int64_t *offsets, const int32_t *
     c->nblocks = nblocks;
     c->nfull = nfull;
     c->xact = xact;
+    c->wq_grid = wq_grid;
     if (const char *pe = std::getenv("HMMBW_PRIO")) c->prio = std::atoi(pe);
     c->has_obs = true;
     return ensure_zf(c);

@@ -175,6 +175,10 @@ struct EArgs {
     // second wave on their SIMDs (cfg3 34.5-34.7 us per iteration against 36.0-36.8 at 0, two interleaved
     // rounds; no effect without extra waves, e.g. 12,500 sequences); 1 = for the full workgroups' waves
     int prio;
+    // wide work queue (k_estep_mfma<..., WQ>): [0] next unit, [1] workgroups done; per-tile forward flags
+    unsigned *wq;
+    unsigned *wq_flag;
+    int wq_units;  // tiles
 };
 
 // Grouped launch (k_estep_small_group): per-model arguments and first workgroups (start[nm] = grid)

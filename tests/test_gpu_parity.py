@@ -158,6 +158,38 @@ def test_training_vs_oracle_random(N, K, topology, safe, oracle):
     assert_params(p2, ref.pi, "pi")
 
 
+@pytest.mark.parametrize("N,equal", [(24, False), (64, False), (64, True)])
+@pytest.mark.parametrize("wq", ["1", "0"])
+def test_wide_work_queue_vs_oracle(N, equal, wq, oracle, monkeypatch):
+    """The wide E-step with more 16-sequence tiles than CUs runs as a work queue of forward and backward
+    sweeps (estep_mfma.hpp, WQ; HMMBW_WIDE_WQ=1 forces it above one tile per CU, 0 keeps one tile per
+    workgroup): 3 EM iterations against
+    the oracle (hmm_training.py:351-514), ragged and equal lengths, both forms."""
+    import torch
+    from hmm_training_amd.engine import BaumWelchEngine, to_csr
+    monkeypatch.setenv("HMMBW_WIDE_WQ", wq)
+    ncu = torch.cuda.get_device_properties(0).multi_processor_count
+    R = 16 * ncu + 16 * 21 + 5  # tiles > CUs (the queue form), the last tile partly filled
+    K = 64
+    rng = np.random.default_rng(31 * N + int(equal))
+    obs, pi, A, B = random_problem(rng, N, K, R=R, tmax=24, topology="dense")
+    if equal:
+        obs = [rng.integers(0, K, size=24) for _ in range(R)]
+    off, sym = to_csr(obs)
+    ref = oracle.hmm_training(off, sym.astype(np.int64), N, K, 1e-9, 3, pi, A, B)
+    with BaumWelchEngine(N, K, topology="dense") as eng:
+        eng.set_observations(obs)
+        eng.set_params(pi, A, B)
+        trace = []
+        eng.train(1e-9, 3, lambda k, L, df: trace.append(L))
+        assert_ll(trace, ref.trace_L)
+        assert_ll(eng.loglik(), ref.logP)
+        p2, A2, B2 = eng.params(normalise=True)
+    assert_params(A2, ref.A, "A")
+    assert_params(B2, ref.B, "B")
+    assert_params(p2, ref.pi, "pi")
+
+
 @pytest.mark.parametrize("topology", ["dense", "left_to_right"])
 def test_estep_statistics_vs_oracle(topology, oracle):
     import torch
