@@ -182,6 +182,15 @@ def test_split_iteration_multirank_vs_oracle(hip, oracle_mt, N, K, topology, R, 
         assert_params(p2, ref.pi, f"pi rank {r}")
 
 
+def test_split_iteration_multirank_work_queue_vs_oracle(hip, oracle_mt, monkeypatch):
+    """The wide work-queue E-step (more tiles than CUs per rank, HMMBW_WIDE_WQ=1) on the fused
+    multi-rank path: the last backward unit folds the ranks' log-likelihood pairs over every tile."""
+    import torch
+    monkeypatch.setenv("HMMBW_WIDE_WQ", "1")
+    ncu = torch.cuda.get_device_properties(0).multi_processor_count
+    test_split_iteration_multirank_vs_oracle(hip, oracle_mt, 40, 96, "dense", 2 * 16 * (ncu + 9), 40, 2)
+
+
 def test_split_iteration_stat_copies_and_payload(hip):
     """Fused payload = copies * statistics + one pair per rank, 256-B aligned, identical on every rank."""
     d = load("n8_k256_t200")
