@@ -44,6 +44,9 @@ constexpr int kTileSeqs = 16;  // sequences per tile = MFMA columns
 #define HMMBW_GAMMA_NT 1
 #endif
 // alpha_hat (written by the forward, read once by the backward) likewise: E-step 1,480-1,488 -> 1,476-1,481 us
+#ifndef HMMBW_WQ_WT  // A/B: the work queue passes alpha_hat and s_t with agent-scope stores / loads (no fences)
+#define HMMBW_WQ_WT 0
+#endif
 #ifndef HMMBW_ALPHA_NT
 #define HMMBW_ALPHA_NT 1
 #endif
@@ -267,13 +270,18 @@ __global__ void __launch_bounds__(NT * 64, 2) k_estep_mfma(EArgs a) {  // 2 wave
             if (!WIDE_ABL(a, 8)) {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    if constexpr (HMMBW_ALPHA_NT) __builtin_nontemporal_store(z[r], &ckw[((long long)t * NT * 4 + r) * 64]);
+                    if constexpr (WQ && HMMBW_WQ_WT)
+                        __hip_atomic_store(&ckw[((long long)t * NT * 4 + r) * 64], z[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    else if constexpr (HMMBW_ALPHA_NT) __builtin_nontemporal_store(z[r], &ckw[((long long)t * NT * 4 + r) * 64]);
                     else ckw[((long long)t * NT * 4 + r) * 64] = z[r];
                 }
             }
             // every wave computes the same s_t from all NP states: one lane group stores it (STEADY: all
             // lanes, the same value to the same 16 words, so the store needs no exec branch)
-            if (STEADY || (m == 0 && g == 0)) ew[t * kTileSeqs] = sc;
+            if (STEADY || (m == 0 && g == 0)) {
+                if constexpr (WQ && HMMBW_WQ_WT) __hip_atomic_store(&ew[t * kTileSeqs], sc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                else ew[t * kTileSeqs] = sc;
+            }
         }
         if (!WIDE_ABL(a, 16)) __syncthreads();
     };
@@ -317,12 +325,13 @@ __global__ void __launch_bounds__(NT * 64, 2) k_estep_mfma(EArgs a) {  // 2 wave
             }
         }
         __syncthreads();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        if constexpr (!HMMBW_WQ_WT) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         if (Tw > 0) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const double *q = &ckw[((long long)(Tw - 1) * NT * 4 + r) * 64];
-                if constexpr (HMMBW_ALPHA_NT) z[r] = __builtin_nontemporal_load(q);
+                if constexpr (HMMBW_WQ_WT) z[r] = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                else if constexpr (HMMBW_ALPHA_NT) z[r] = __builtin_nontemporal_load(q);
                 else z[r] = *q;
             }
         }
@@ -386,12 +395,18 @@ __global__ void __launch_bounds__(NT * 64, 2) k_estep_mfma(EArgs a) {  // 2 wave
         unsigned dring[2];  // gamma row of step t in slot t % 2, loaded in the visit before consume(t)
         f64x4 zs;  // z_t masked to the regular steps: gamma_t of the step that consumes the image
         f64x4 accn;  // beta of the next step to consume: its own-block MFMAs, issued by publish
+        auto ldew = [&](int t) HMMBW_AI -> int {
+            if constexpr (WQ && HMMBW_WQ_WT) return __hip_atomic_load(&ew[t * kTileSeqs], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            else return ew[t * kTileSeqs];
+        };
         auto ldz = [&](int t) HMMBW_AI -> f64x4 {
             f64x4 v;
             if (WIDE_ABL(a, 8)) return f64x4{0.5, 0.5, 0.5, 0.5};
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                if constexpr (HMMBW_ALPHA_NT) v[r] = __builtin_nontemporal_load(&ckw[((long long)t * NT * 4 + r) * 64]);
+                if constexpr (WQ && HMMBW_WQ_WT)
+                    v[r] = __hip_atomic_load(&ckw[((long long)t * NT * 4 + r) * 64], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                else if constexpr (HMMBW_ALPHA_NT) v[r] = __builtin_nontemporal_load(&ckw[((long long)t * NT * 4 + r) * 64]);
                 else v[r] = ckw[((long long)t * NT * 4 + r) * 64];
             }
             return v;
@@ -485,7 +500,7 @@ __global__ void __launch_bounds__(NT * 64, 2) k_estep_mfma(EArgs a) {  // 2 wave
                 if (STEADY || t >= 1) dring[(k + 1) & 1] = gdw[(t - 1) * kTileSeqs];  // row of step t - 1
                 if (STEADY || t >= 2) {
                     bring1[(k + 1) & 1] = emis(k >= 1 ? sym_of(pc, k - 1) : sym_of(pp, kChunk - 1));  // b(o_{t-1})
-                    sring[(k + 1) & 1] = ew[(t - 1) * kTileSeqs];                                   // s_{t-1}
+                    sring[(k + 1) & 1] = ldew(t - 1);  // s_{t-1}
                 }
                 if (STEADY || t >= 3) zring[(k + 1) & 1] = ldz(t - 3);
             }
@@ -502,7 +517,7 @@ __global__ void __launch_bounds__(NT * 64, 2) k_estep_mfma(EArgs a) {  // 2 wave
             }
             // b(o_{ttop-1}), s_{ttop-1} for the first visit (slot 1: ttop - 1 is odd)
             bring1[1] = emis(sym_of(pc, kChunk - 1));
-            sring[1] = ew[(ttop - 1) * kTileSeqs];
+            sring[1] = ldew(ttop - 1);
             dring[1] = gdw[(ttop - 1) * kTileSeqs];
             // chunks [1, cs] have every step t <= Tw - 2 (c * kChunk + kChunk - 1 <= Tw - 2)
             const int cs = Tw >= kChunk + 1 ? (Tw - kChunk - 1) / kChunk : 0;
@@ -548,7 +563,8 @@ __global__ void __launch_bounds__(NT * 64, 2) k_estep_mfma(EArgs a) {  // 2 wave
         if (do_f) {  // the tile's log P pair, then the release of alpha_hat and s_t to its backward unit
             __syncthreads();
             block_ll_partial(lp, ll_valid, sRed + NT * kTileSeqs, a.llpart + 2 * tile);
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            if constexpr (HMMBW_WQ_WT) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the stores have landed
+            else __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
             __syncthreads();
             if (tid == 0) __hip_atomic_store(a.wq_flag + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         } else if (a.rank_ll != nullptr) {
