@@ -44,8 +44,12 @@ constexpr int kTileSeqs = 16;  // sequences per tile = MFMA columns
 #define HMMBW_GAMMA_NT 1
 #endif
 // alpha_hat (written by the forward, read once by the backward) likewise: E-step 1,480-1,488 -> 1,476-1,481 us
-#ifndef HMMBW_WQ_WT  // A/B: the work queue passes alpha_hat and s_t with agent-scope stores / loads (no fences)
-#define HMMBW_WQ_WT 0
+// The work queue hands alpha_hat and s_t from the forward unit to the backward unit with agent-scope
+// stores / loads (write-through past the non-coherent XCD L2s; the flag follows vmcnt(0)) instead of a
+// release fence (an XCD-wide L2 write-back per forward unit) and an acquire (an L2 invalidate per
+// backward unit): whole cfg5 11.78 -> 11.57 ms per iteration (profiles/r4/wide_work_queue_ab.txt).
+#ifndef HMMBW_WQ_WT
+#define HMMBW_WQ_WT 1
 #endif
 #ifndef HMMBW_ALPHA_NT
 #define HMMBW_ALPHA_NT 1
