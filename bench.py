@@ -22,15 +22,15 @@ launcher, --gpus must equal WORLD_SIZE.  --dry-run runs the launcher/rendezvous/
 with no GPU work (CPU tests).
 
 Prints ONE JSON line (rank 0) with the driver's fields plus:
-  roofline     — the BINDING ceiling of the E-step launch (roofline_bounds): of the bounds that apply,
-                 each written as achieved / peak of one resource, the one with the largest fraction:
-                 hbm (calibrated PMC bytes per launch from profiles/ over the kernel time, 8 TB/s),
-                 valu (all VALU instructions spread over the 1,024 SIMDs), simd_valu (the busiest SIMD's
-                 VALU pipe: ceil(waves / 1,024) waves' instructions, 4 cycles each at 2.4 GHz), and on
-                 the wide path (N > 16, cfg5) mfma / simd_mfma (the fp64 matrix pipe, 64 cycles per
-                 v_mfma_f64_16x16x4).  The kernel time is HIP events on the engine stream.  The SURVEY
-                 §8(d) byte model (B_u = 24T + 16NT + 8 per sequence) is kept as effective_bw_frac: it
-                 charges an alpha_hat round trip the kernels never make, so it can exceed 1.
+  roofline     — SURVEY §8(d) for the dominant launch: algorithmic work over the kernel's launch duration
+                 (HIP events on the engine stream) against the bounding resource's peak: bound "hbm",
+                 B_u = 24T + 16NT + 8 bytes per sequence vs 8 TB/s on the small kernels (a fixed conversion
+                 that charges an alpha_hat round trip the kernels never make, so frac can exceed 1); bound
+                 "mfma", 8 N^2 T flops per sequence vs 78.6 TF fp64 on the wide path.  traffic = calibrated
+                 PMC HBM bytes per launch (profiles/).  binding = the tightest ceiling the counters measure
+                 (roofline_bounds: hbm measured bytes, valu, simd_valu, cu_lds, mfma, simd_mfma; the busiest
+                 SIMD and CU counted on the engine's launch map), with the profile's provenance (file,
+                 collection time, kernel-source hash, fresh = collected on these kernels).
   cpu_baseline — the oracle C restatement (oracle/bw_oracle.c, log domain like the reference) with
                  OpenMP over utterances on the host cores this process may use, timed on a bounded
                  sample of the same workload (rank 0, N=1 only), with its ratio to the reference's
@@ -163,18 +163,47 @@ def mfma_flops_issued(T, N):
     return 6 * N * N * T  # what k_estep_mfma issues: forward 2N^2, backward 2N^2, xi 2N^2 per step
 
 
+def kernel_source_hash() -> str:
+    """sha256 (first 16 hex digits) of the engine's kernel sources (hmm_training_amd/csrc/*, include/hmmbw.h):
+    the profile summaries record the hash of the tree they were collected on, so a bound read from a profile
+    of older kernels shows up as stale in the bench line."""
+    import hashlib
+    h = hashlib.sha256()
+    paths = sorted(glob.glob(os.path.join(ROOT, "hmm_training_amd", "csrc", "*"))) + [os.path.join(ROOT, "include", "hmmbw.h")]
+    for p in paths:
+        with open(p, "rb") as fh:
+            h.update(os.path.basename(p).encode() + b"\0" + fh.read())
+    return h.hexdigest()[:16]
+
+
+def _provenance(d, path):
+    """Where a committed profile summary came from: file, collection time and kernel-source hash (fresh =
+    collected on the kernel sources of this tree)."""
+    src = d.get("kernel_src_sha16")
+    return {"source": os.path.relpath(path, ROOT), "collected_utc": d.get("collected_utc"), "kernel_src_sha16": src,
+            "fresh": src == kernel_source_hash() if src else None}
+
+
 def find_traffic(cfg_key):
-    """Per-launch HBM bytes of the E-step kernel from a committed PMC summary for this config."""
+    """Per-launch HBM bytes of the E-step kernel from a committed PMC summary for this config (the newest
+    round's, profiles/rN sorted by round number)."""
     best = None
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "**", "*traffic*.json"), recursive=True)):
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "**", "*traffic*.json"), recursive=True), key=_round_key):
         try:
             with open(path) as fh:
                 d = json.load(fh)
         except Exception:
             continue
         if d.get("config_key") == cfg_key and d.get("hbm_bytes_per_launch"):
-            best = (float(d["hbm_bytes_per_launch"]), os.path.relpath(path, ROOT))
+            best = (float(d["hbm_bytes_per_launch"]), os.path.relpath(path, ROOT), _provenance(d, path))
     return best
+
+
+def _round_key(path):
+    """Sort key of a profiles/rN/... path: by round number, then name."""
+    rel = os.path.relpath(path, os.path.join(ROOT, "profiles"))
+    head = rel.split(os.sep)[0]
+    return (int(head[1:]) if head[:1] == "r" and head[1:].isdigit() else -1, rel)
 
 
 SIMDS = 1024       # 256 CUs x 4 SIMDs (MI355X_MICROARCH.md chip-level parameters)
@@ -188,7 +217,7 @@ MFMA_F64_FLOPS = 2 * 16 * 16 * 4
 def find_issue(cfg_key):
     """VALU instructions per E-step launch and the loaded clock from a committed SQ summary."""
     best = None
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "**", "sq_*.json"), recursive=True)):
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "**", "sq_*.json"), recursive=True), key=_round_key):
         try:
             with open(path) as fh:
                 d = json.load(fh)
@@ -202,23 +231,44 @@ def find_issue(cfg_key):
                         "valu_fp64_per_launch": k.get("valu_fp64_insts"),
                         "mfma_busy_cycles": k.get("SQ_VALU_MFMA_BUSY_CYCLES"),
                         "lds_array_cycles": k.get("SQ_LDS_IDX_ACTIVE"),
-                        "clock_ghz_grbm_estimate": k.get("clock_ghz"), "source": os.path.relpath(path, ROOT)}
+                        "waves_counted": k.get("SQ_WAVES"),
+                        "clock_ghz_grbm_estimate": k.get("clock_ghz"), "source": os.path.relpath(path, ROOT),
+                        "provenance": _provenance(k, path)}
     return best
 
 
-def engine_waves(R, N):
-    """Active waves of one E-step launch and the pigeonhole minimum of the busiest SIMD's waves.
-    Small kernels (N <= 16): 64 / G sequences per wave, G = pow2ceil(N); wide (16 < N <= 64): tiles of
-    16 sequences with NP / 16 waves each (hmmbw.hip, hmmbw_set_observations)."""
+CUS = SIMDS // 4
+
+
+def engine_waves(R, N, lmap=None):
+    """(active waves, waves on the busiest SIMD, waves on the busiest CU) of one E-step launch.
+
+    With the engine's launch map (BaumWelchEngine.launch_map, HMMBW_INFO_*: the spread map of the small
+    kernels puts one full 4-wave workgroup on every CU, then the waves past one per SIMD into workgroups of
+    `extra_waves` active waves) the busiest CU and SIMD are counted on that map, workgroup i placed on CU
+    i mod 256 (dispatch order; the kernels admit two workgroups per CU) and a CU's waves spread over its 4
+    SIMDs.  Without it (CPU tests): small kernels 64 / G sequences per wave, wide tiles of 16 sequences
+    with NP / 16 waves, and the pigeonhole minimum ceil(waves / 1,024) per SIMD, ceil(waves / 256) per CU."""
+    if lmap and lmap.get("waves") and not lmap.get("work_queue"):
+        waves, nwg, wpw = lmap["waves"], lmap["workgroups"], lmap["waves_per_workgroup"]
+        full, extra = min(lmap["full_workgroups"], nwg), lmap["extra_waves"] or wpw
+        cu = [0] * CUS
+        left = waves
+        for i in range(nwg):
+            w = min(wpw if i < full else extra, left)
+            left -= w
+            cu[i % CUS] += w
+        wcu = max(cu)
+        return waves, -(-wcu // 4), wcu
     if N <= 16:
         G = 2 if N <= 2 else 4 if N <= 4 else 8 if N <= 8 else 16
         waves = -(-R // (64 // G))
     else:
         waves = -(-R // 16) * (-(-N // 16))
-    return waves, -(-waves // SIMDS)
+    return waves, -(-waves // SIMDS), -(-waves // CUS)
 
 
-def roofline_bounds(R, T, N, kern_s, traffic, issue, estep_s=None):
+def roofline_bounds(R, T, N, kern_s, traffic, issue, estep_s=None, lmap=None):
     """Every ceiling that applies to the dominant launch, each as achieved / peak of ONE resource, so every
     frac is <= 1 when the measurement and the model are right; the binding bound is the largest frac.
 
@@ -227,20 +277,25 @@ def roofline_bounds(R, T, N, kern_s, traffic, issue, estep_s=None):
                2.4 GHz max clock: on a SIMD-32 a wave64 fp64 add / mul / fma / transcendental takes 4 cycles
                (half the fp32 rate), every other VALU instruction 2 (MI355X_MICROARCH.md, SIMD-32), with the
                fp64 share from the SQ_INSTS_VALU_{ADD,MUL,FMA,TRANS}_F64 counters.
-    simd_valu  the busiest SIMD: by pigeonhole some SIMD runs w = ceil(waves / 1,024) waves and must issue
+    simd_valu  the busiest SIMD: it runs w waves (the launch map's busiest SIMD, engine_waves) and must issue
                all their VALU instructions on its one VALU pipe, max(w x (4 n64 + 2 (n - n64)), 4 n) cycles
                for n VALU instructions per wave of which n64 fp64 (a single wave issues at most every 4
                cycles); achieved / peak = that time / the kernel time, written as an issue rate.
+    cu_lds     the busiest CU's LDS array (shared by its 4 SIMDs): its waves x the LDS-array cycles per wave
+               (SQ_LDS_IDX_ACTIVE, bank-conflict cycles included) at the max clock / the kernel time.
     mfma, simd_mfma  (wide path) the same for the fp64 matrix pipe: every wave issues 48 dependent-block
                v_mfma_f64_16x16x4 per step (forward 4NT, backward 4NT, xi 4NT at NT = 4), 64 cycles each.
     """
-    waves, wmax = engine_waves(R, N)
+    waves, wmax, wcu = engine_waves(R, N, lmap)
     t_clock = CLOCK_MAX_GHZ * 1e9
-    out = {"waves_per_launch": waves, "waves_on_busiest_simd": wmax, "clock_ghz": CLOCK_MAX_GHZ}
+    out = {"waves_per_launch": waves, "waves_on_busiest_simd": wmax, "waves_on_busiest_cu": wcu,
+           "wave_map": ("engine launch map (HMMBW_INFO_*), workgroup i on CU i mod 256" if lmap and not lmap.get("work_queue")
+                        else "pigeonhole (no launch map)"),
+           "clock_ghz": CLOCK_MAX_GHZ}
     if traffic and kern_s > 0:
         ach = traffic[0] / kern_s / 1e9
         out["hbm"] = {"achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
-                      "bytes_per_launch": traffic[0], "source": traffic[1]}
+                      "bytes_per_launch": traffic[0], "source": traffic[1], "provenance": traffic[2]}
     if N > 16:
         nt = -(-N // 16)
         mfma_wave = 3 * 4 * nt * T  # per step: forward 4NT, backward 4NT, xi NT x 4 (estep_mfma.hpp)
@@ -262,23 +317,21 @@ def roofline_bounds(R, T, N, kern_s, traffic, issue, estep_s=None):
         t_bal = cyc_all / SIMDS / t_clock
         out["valu"] = {"achieved": t_bal / kern_s, "peak": 1.0, "unit": "fraction of SIMD VALU issue cycles (mean)",
                        "frac": t_bal / kern_s, "t_bound_us": 1e6 * t_bal, "valu_per_launch": n_all,
-                       "valu_fp64_per_launch": n64, "source": issue["source"]}
+                       "valu_fp64_per_launch": n64, "source": issue["source"], "provenance": issue["provenance"]}
         nw, n64w = n_all / waves, n64 / waves
         cyc_simd = max(wmax * (VALU_CYCLES * n64w + VALU_CYCLES_32 * (nw - n64w)), VALU_CYCLES * nw)
         t_simd = cyc_simd / t_clock
         out["simd_valu"] = {"achieved": t_simd / kern_s, "peak": 1.0,
                             "unit": "fraction of the busiest SIMD's VALU issue cycles", "frac": t_simd / kern_s,
                             "t_bound_us": 1e6 * t_simd, "valu_per_wave": nw, "valu_fp64_per_wave": n64w,
-                            "source": issue["source"]}
+                            "waves_on_busiest_simd": wmax, "source": issue["source"], "provenance": issue["provenance"]}
     if issue and kern_s > 0 and N <= 16 and issue.get("lds_array_cycles"):
-        # the busiest CU's LDS array (shared by its 4 SIMDs): by pigeonhole some CU runs ceil(waves / 256)
-        # waves; SQ_LDS_IDX_ACTIVE = every LDS-array cycle of the launch, bank-conflict cycles included
-        cus = SIMDS // 4
-        wcu = -(-waves // cus)
+        # SQ_LDS_IDX_ACTIVE = every LDS-array cycle of the launch, bank-conflict cycles included, per active wave
         t_lds = wcu * issue["lds_array_cycles"] / waves / t_clock
         out["cu_lds"] = {"achieved": t_lds / kern_s, "peak": 1.0, "unit": "fraction of the busiest CU's LDS-array cycles",
                          "frac": t_lds / kern_s, "t_bound_us": 1e6 * t_lds, "waves_on_busiest_cu": wcu,
-                         "lds_cycles_per_wave": issue["lds_array_cycles"] / waves, "source": issue["source"]}
+                         "lds_cycles_per_wave": issue["lds_array_cycles"] / waves, "source": issue["source"],
+                         "provenance": issue["provenance"]}
     cands = {k: v for k, v in out.items() if isinstance(v, dict) and "frac" in v}
     out["binding"] = max(cands, key=lambda k: cands[k]["frac"]) if cands else None
     return out
@@ -474,8 +527,7 @@ def main(argv=None):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         ev0.record()
-        for _ in range(steps):
-            enqueue(1)
+        enqueue(steps)  # one hmmbw_iterate(steps): the host enqueues the K launches back to back
         ev1.record()
         torch.cuda.synchronize()
         if world > 1:
@@ -539,6 +591,39 @@ def main(argv=None):
             n_iter[0] = 0
         else:
             legs[other] = r2
+    agree = None
+    if len(legs) > 1:
+        # both all-reduces must give the same EM run before either is a headline: the same few iterations
+        # from the same parameters on each, L traces (hmm_training.py:503) compared at rtol 1e-9; a leg that
+        # disagrees with RCCL (e.g. a peer exchange that is not coherent over xGMI) is dropped
+        traces = {}
+        for kind in legs:
+            eng.set_allreduce(kind)
+            eng.set_params(pi, A, B)
+            eng.reset(0.0, 3)
+            eng.enqueue_iterations(3, stats)
+            try:
+                traces[kind] = [L for L, _ in eng.status(0, 3)[1]]
+            except Exception as e:  # noqa: BLE001 - a device-side failure of the check drops that leg
+                traces[kind] = str(e)
+        ref_t = traces.get("rccl")
+        agree = {}
+        for kind, tr in traces.items():
+            ok = isinstance(tr, list) and isinstance(ref_t, list) and np.allclose(tr, ref_t, rtol=1e-9, atol=0.0)
+            agree[kind] = bool(ok)
+            if kind != "rccl" and not ok:
+                failed[kind] = f"L trace differs from the RCCL leg's: {tr} vs {ref_t}"
+                legs.pop(kind)
+        if world > 1:  # every rank drops the same legs
+            keep = torch.tensor([1 if k in legs else 0 for k in ("rccl", "peer")], dtype=torch.int32,
+                                device=f"cuda:{device}" if args.dist_backend == "nccl" else "cpu")
+            dist.all_reduce(keep, op=dist.ReduceOp.MIN)
+            for i, k in enumerate(("rccl", "peer")):
+                if k in legs and int(keep[i]) == 0:
+                    legs.pop(k)
+                    failed.setdefault(k, "another rank's check failed")
+        eng.reset(0.0, 1 << 40)
+        n_iter[0] = 0
     # the headline is the faster leg (both run the full EM iteration; config.allreduce names it)
     best = max(legs, key=lambda k: -legs[k]["elapsed"])
     L = legs[best]
@@ -569,32 +654,41 @@ def main(argv=None):
     traffic = find_traffic(cfg_key)
     issue = find_issue(cfg_key)
     estep_s = (est_ms / est_n / 1000.0) if est_n else None
-    bounds = roofline_bounds(R, T, N, kern_s, traffic, issue, estep_s)
-    # The roofline is the binding ceiling among the bounds that apply (largest achieved / peak).  The
-    # SURVEY §8(d) byte model (B_u = 24T + 16NT + 8 per sequence over the launch) is kept beside it as
-    # effective_bw_frac: it charges an alpha_hat HBM round trip the checkpoint-and-recompute kernels never
-    # make, so on the small kernels it exceeds 1 and bounds nothing.
+    lmap = eng.launch_map()
+    bounds = roofline_bounds(R, T, N, kern_s, traffic, issue, estep_s, lmap)
+    # The roofline (the task's contract and SURVEY §8(d)): ALGORITHMIC work per launch over the kernel's
+    # average launch duration against the peak of the bounding resource.  Small kernels: HBM, B_u = 24T +
+    # 16NT + 8 bytes per sequence (a fixed conversion: it charges an alpha_hat round trip the
+    # checkpoint-and-recompute kernels never make, so frac can exceed 1).  Wide path: the fp64 matrix
+    # pipe, 8 N^2 T flops per sequence over the E-step kernel.  `binding` is the tightest ceiling the
+    # counters measure (largest achieved / peak among `bounds`, each <= 1 when measurement and model are
+    # right), with the profile it came from and whether that profile was collected on these kernels.
     b = bounds.get(bounds.get("binding") or "", None)
     if wide:
-        eff = flops_per_sequence(T, N) * R / kern_s / 1e12 if kern_s > 0 else float("nan")
-        eff_model = {"effective_tflops_8N2T": eff, "effective_frac_8N2T": eff / FP64_MFMA_PEAK_TFS,
-                     "issued_frac_6N2T": mfma_flops_issued(T, N) * R / kern_s / 1e12 / FP64_MFMA_PEAK_TFS,
-                     "flops_per_launch_algorithmic": flops_per_sequence(T, N) * R}
-        eff_frac = eff / FP64_MFMA_PEAK_TFS
+        t_e = estep_s if estep_s else kern_s
+        ach = flops_per_sequence(T, N) * R / t_e / 1e12 if t_e > 0 else float("nan")
+        model = {"bound": "mfma", "achieved": ach, "peak": FP64_MFMA_PEAK_TFS, "unit": "TFLOP/s",
+                 "frac": ach / FP64_MFMA_PEAK_TFS, "units_per_launch": R,
+                 "work_per_unit": f"{flops_per_sequence(T, N)} flops (SURVEY §8(d): 8 N^2 T per sequence)",
+                 "issued_frac_6N2T": mfma_flops_issued(T, N) * R / t_e / 1e12 / FP64_MFMA_PEAK_TFS,
+                 "kernel": "k_estep_mfma", "kernel_ms": 1e3 * t_e}
     else:
-        eff = bu * R / kern_s / 1e9 if kern_s > 0 else float("nan")
-        eff_model = {"effective_bw_gbs": eff, "bytes_per_launch_algorithmic": bu * R,
-                     "model": "SURVEY §8(d): 24T + 16NT + 8 bytes per sequence"}
-        eff_frac = eff / HBM_PEAK_GBS
-    roof = {"bound": bounds.get("binding") or ("mfma" if wide else "hbm"),
-            "achieved": b["achieved"] if b else None, "peak": b["peak"] if b else None,
-            "unit": b["unit"] if b else None, "frac": b["frac"] if b else None,
-            "traffic": traffic[0] if traffic else None,
+        ach = bu * R / kern_s / 1e9 if kern_s > 0 else float("nan")
+        model = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
+                 "units_per_launch": R,
+                 "work_per_unit": f"{bu} bytes (SURVEY §8(d): 24 T + 16 N T + 8 per sequence)",
+                 "kernel": "k_estep_small", "kernel_ms": 1e3 * kern_s}
+    roof = {"bound": model["bound"], "achieved": model["achieved"], "peak": model["peak"], "unit": model["unit"],
+            "frac": model["frac"], "traffic": traffic[0] if traffic else None,
+            "model": model,
             "kernel": "k_estep_mfma + k_bnum_gather (E-step)" if wide else "k_estep_small (E-step)",
             "kernel_ms": kern_s * 1000.0, "kernel_time_source": kern_src,
-            "effective_bw_frac": eff_frac, "byte_model": eff_model,
+            "binding": ({"resource": bounds["binding"], **{k: b[k] for k in ("achieved", "peak", "unit", "frac")},
+                         "t_bound_us": b.get("t_bound_us"), "provenance": b.get("provenance")} if b else None),
             "hbm_frac_measured": bounds["hbm"]["frac"] if "hbm" in bounds else None,
-            "bounds": bounds, "traffic_source": traffic[1] if traffic else None,
+            "traffic_provenance": traffic[2] if traffic else None,
+            "kernel_src_sha16": kernel_source_hash(),
+            "bounds": bounds, "launch_map": lmap,
             "gpu_ms_per_step": gpu_ms_step,
             "kernel_ms_per_launch_events": kern_ms / kern_n if kern_n else None}
 
@@ -631,7 +725,13 @@ def main(argv=None):
                                   "allreduce_us_per_iter": 1000.0 * v["ar_ms"] / v["ar_n"] if v["ar_n"] else None,
                                   "kernel_ms_per_launch_events": v["kern_ms"] / v["kern_n"] if v["kern_n"] else None}
                               for k, v in legs.items()},
-                     "legs_failed": failed}
+                     "legs_failed": failed, "legs_agree": agree,
+                     "legs_detail": {k: {"payload_bytes": eng.comm_payload_bytes() if eng.native_comm else 8 * eng.stats_len,
+                                         "peer_chunks": eng.peer_chunks() if k == "peer" else None,
+                                         "peer_flags_written_and_polled_per_rank_per_iter": (
+                                             world * eng.peer_chunks() if k == "peer" else None),
+                                         "collectives_per_iter": 1}
+                                     for k in legs}}
             if world > 1 else None,
             "synced": synced,
             "upload_s": upload_s,

@@ -39,9 +39,9 @@ EXPORTED = (
     "hmmbw_group_timing", "hmmbw_vq_encode", "hmmbw_comm_unique_id", "hmmbw_comm_init",
     "hmmbw_comm_probe", "hmmbw_comm_info", "hmmbw_comm_payload", "hmmbw_iterate_begin", "hmmbw_iterate_end",
     "hmmbw_cache_trim", "hmmbw_timing_split", "hmmbw_peer_region", "hmmbw_peer_ipc_handle", "hmmbw_peer_open",
-    "hmmbw_peer_attach", "hmmbw_allreduce_kind", "hmmbw_status_live_wait",
+    "hmmbw_peer_attach", "hmmbw_allreduce_kind", "hmmbw_status_live_wait", "hmmbw_get_option",
 )
-ABI_VERSION = 4
+ABI_VERSION = 5
 OPT_SAFE_SCALING = 1
 OPT_ABLATE = 2
 OPT_STAT_COPIES = 3
@@ -50,6 +50,15 @@ OPT_DETERMINISTIC = 7
 OPT_ALLREDUCE = 8
 OPT_PEER_TIMEOUT_MS = 9
 OPT_LIVE_STATUS = 10
+OPT_WQ_TIMEOUT_MS = 11
+OPT_WIDE_WQ = 12
+INFO_WIDE_WQ_ACTIVE = 101
+INFO_WAVES = 102
+INFO_WORKGROUPS = 103
+INFO_WAVES_PER_WORKGROUP = 104
+INFO_FULL_WORKGROUPS = 105
+INFO_EXTRA_WAVES = 106
+INFO_PEER_CHUNKS = 107
 ALLREDUCE = {"rccl": 0, "peer": 1}
 
 
@@ -112,6 +121,7 @@ def _declare(lib):
         "hmmbw_peer_attach": (ctypes.c_int, [c_ctx, ctypes.c_void_p, ctypes.c_int64]),
         "hmmbw_allreduce_kind": (ctypes.c_int, [c_ctx, P(ctypes.c_int)]),
         "hmmbw_set_option": (ctypes.c_int, [c_ctx, ctypes.c_int, ctypes.c_int64]),
+        "hmmbw_get_option": (ctypes.c_int, [c_ctx, ctypes.c_int, P(ctypes.c_int64)]),
         "hmmbw_vq_encode": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int,
                                            ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
                                            ctypes.c_void_p]),

@@ -319,18 +319,37 @@ __global__ void __launch_bounds__(NT * 64, 2) k_estep_mfma(EArgs a) {  // 2 wave
         if (full) forward(std::false_type{});
         else forward(std::true_type{});
     } else if constexpr (WQ) {
-        // backward unit: wait for the tile's forward (bounded: it runs on a resident workgroup), then
-        // z_{Tw-1} (masked per sequence, as the forward left it in its registers) from alpha_hat
+        // backward unit: wait for the tile's forward (it runs on a resident workgroup, so the wait ends),
+        // then z_{Tw-1} (masked per sequence, as the forward left it in its registers) from alpha_hat.
+        // The wait is bounded (HMMBW_OPT_WQ_TIMEOUT_MS, wall-clock ticks from the host): past it the unit
+        // records HMMBW_E_TIMEOUT in the iteration state, stops EM (done: the gather, the M-step and every
+        // later launch become no-ops, the status calls return the error) and skips its backward sweep, as
+        // the peer all-reduce does; it never reads an alpha_hat that may not be there.  A 0-ms bound
+        // expires before the first look at the flag.
+        __shared__ int s_ok;
         if (tid == 0) {
             const unsigned long long t0 = wall_clock64();
-            while (__hip_atomic_load(a.wq_flag + tile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
-                if (wall_clock64() - t0 > 1000000000ull) break;  // 10 s: never hang the device
+            int ok = 1;
+            while (true) {
+                if ((long long)(wall_clock64() - t0) >= a.wq_timeout_ticks) {
+                    ok = 0;
+                    break;
+                }
+                if (__hip_atomic_load(a.wq_flag + tile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) break;
                 __builtin_amdgcn_s_sleep(8);
             }
+            if (!ok) {
+                IterState *st = const_cast<IterState *>(a.state);
+                __hip_atomic_store(&st->error, (int)HMMBW_E_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&st->error_src, kErrWorkQueue, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&st->done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            s_ok = ok;
         }
         __syncthreads();
+        do_b = s_ok != 0;
         if constexpr (!HMMBW_WQ_WT) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        if (Tw > 0) {
+        if (do_b && Tw > 0) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const double *q = &ckw[((long long)(Tw - 1) * NT * 4 + r) * 64];

@@ -211,6 +211,7 @@ __device__ __forceinline__ bool peer_reduce_chunk(double *dst, const PeerArgs &P
     if (!ok) {
         if (tid == 0) {
             state->error = HMMBW_E_TIMEOUT;
+            state->error_src = kErrPeer;
             state->done = 1;
         }
         return false;
@@ -267,7 +268,7 @@ __global__ void k_init_state(IterState *st, double eps, long long max_it) {
     st->done = max_it <= 0 ? 1 : 0;
     st->converged = 0;
     st->error = 0;
-    st->pad_ = 0;
+    st->error_src = 0;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -484,6 +485,8 @@ struct hmmbw_ctx {
     unsigned *d_brows = nullptr;
     unsigned *d_wq = nullptr;  // wide work queue (EArgs::wq): 2 counters + a flag per tile, or nullptr
     long long wq_grid = 0;     // its grid (a workgroup per unit: 2 x tiles)
+    int wq_mode = -1;          // HMMBW_OPT_WIDE_WQ: -1 auto (from 4 tiles per CU), 0 off, 1 on (more tiles than CUs)
+    long long wq_timeout_ms = 10000;  // HMMBW_OPT_WQ_TIMEOUT_MS: bound of a backward unit's wait
     uint4 *d_sp = nullptr;
     int *d_ebuf = nullptr;
     // native RCCL communicator (hmmbw_comm_init): the multi-rank hmmbw_iterate all-reduces d_ext
@@ -682,6 +685,7 @@ MArgs make_margs(hmmbw_ctx *c, const hmmbw_ctx::Pending &p) {
 int flush_mstep(hmmbw_ctx *c) {
     if (!c->pend.on) return HMMBW_OK;
     c->pend.on = false;
+    if (c->ablate & 4) return HMMBW_OK;  // diagnostics (HMMBW_OPT_ABLATE bit 2): no separate M-step kernel
     const MArgs m = make_margs(c, c->pend);
     const size_t staged = sizeof(double) * (size_t)c->copy_len();
     const long long nb = (long long)c->N * c->K;
@@ -732,6 +736,34 @@ int ensure_zf(hmmbw_ctx *c) {
     return HMMBW_OK;
 }
 
+// Wide path with many tiles per CU: a workgroup per forward and per backward sweep, taken from a queue
+// in dispatch order (k_estep_mfma<..., WQ>), so the CUs' loads even out in sweeps instead of whole
+// tiles.  Measured (round 4): whole cfg5 (3,125 tiles) 12.06 against 12.37 ms per iteration; the cfg5
+// shard (391 tiles, 1.5 per CU) 2.17 against 1.85 ms: with so few tiles per CU the backward sweeps
+// (0.63 of a tile) start late and form the tail, so by default (HMMBW_OPT_WIDE_WQ = -1) the queue is
+// used from 4 tiles per CU; 1 uses it whenever there are more tiles than CUs, 0 never (the environment
+// variable HMMBW_WIDE_WQ = 0 / 1 gives the default of a new context).  (Re)allocates or frees the queue
+// to match the current observations; the counters and flags start cleared.
+int ensure_wq(hmmbw_ctx *c) {
+    bool want = false;
+    if (c->has_obs && c->wide && !c->det && c->nblocks < (1LL << 30)) {
+        int ncu = 0;
+        (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device);
+        if (ncu > 0 && c->wq_mode != 0) want = c->nblocks > (c->wq_mode == 1 ? ncu : 4LL * ncu);
+    }
+    if (c->d_wq && (!want || c->wq_grid != 2 * c->nblocks)) {
+        sync_ctx(c);
+        dfree(c->d_wq);
+        c->wq_grid = 0;
+    }
+    if (want && !c->d_wq) {
+        if (int rc = dalloc(&c->d_wq, (size_t)c->nblocks + 2)) return rc;
+        HIP_TRY(hipMemset(c->d_wq, 0, sizeof(unsigned) * ((size_t)c->nblocks + 2)));
+        c->wq_grid = 2 * c->nblocks;
+    }
+    return HMMBW_OK;
+}
+
 int plan_estep(hmmbw_ctx *c, bool fwd_only, const IterState *state, double *copies, double *llpart, double *zero,
                long long zero_len, bool merge, Plan *P, double *rank_ll = nullptr, int ncopies = 0) {
     Plan &p = *P;
@@ -763,6 +795,7 @@ int plan_estep(hmmbw_ctx *c, bool fwd_only, const IterState *state, double *copi
             a.wq = c->d_wq;
             a.wq_flag = c->d_wq + 2;
             a.wq_units = (int)c->nblocks;
+            a.wq_timeout_ticks = c->wq_timeout_ms * c->wall_khz;
             if (!p.fn) return fail(HMMBW_E_UNSUPPORTED, "no wide work-queue kernel for N");
         }
     } else {
@@ -960,6 +993,77 @@ void resolve_topology(hmmbw_ctx *c) {
     c->topo = t;
 }
 
+// Memory of the peer receive regions (HMMBW_PEER_MEM).  Other GPUs write payload and flags into a region
+// over xGMI while this GPU's reduce kernel polls it.  coarse (default): hipMalloc, as every multi-rank test
+// on one GPU ran it (in-process and two / four processes over IPC); the writers' stores are system-scope
+// write-through and the reader's loads system-scope.  uncached / finegrained: hipExtMallocWithFlags kinds
+// that no cache holds (as RCCL keeps its flags), taken from a per-device pool that is never returned to the
+// driver.  Measured (round 5): uncached regions allocated and freed per context corrupted the statistics of
+// later contexts in the same process and once ended in an illegal memory access (the suite alone passed),
+// consistent with the allocator handing freed uncached pages to buffers that take fp64 atomics; the pool keeps
+// such pages out of circulation.  Cross-GPU coherence of either kind is unmeasured here (no multi-GPU box).
+struct PeerPool {
+    std::mutex mu;
+    std::vector<std::tuple<int, unsigned, size_t, void *>> free;  // (device, flags, bytes, region)
+    std::map<void *, std::tuple<int, unsigned, size_t>> owned;
+};
+PeerPool &peer_pool() {
+    static PeerPool *p = new PeerPool;  // never destroyed (regions live for the process)
+    return *p;
+}
+
+int peer_region_alloc(hmmbw_ctx *c, size_t b) {
+    const char *pm = std::getenv("HMMBW_PEER_MEM");
+    const std::string kind = pm ? pm : "coarse";
+    if (kind == "coarse") {
+        HIP_TRY(hipMalloc(reinterpret_cast<void **>(&c->d_peer), b));
+        return HMMBW_OK;
+    }
+    if (kind != "uncached" && kind != "finegrained")
+        return fail(HMMBW_E_INVALID, "HMMBW_PEER_MEM must be coarse, uncached or finegrained");
+    const unsigned fl = kind == "finegrained" ? hipDeviceMallocFinegrained : hipDeviceMallocUncached;
+    PeerPool &pp = peer_pool();
+    std::lock_guard<std::mutex> lk(pp.mu);
+    for (size_t i = 0; i < pp.free.size(); ++i) {
+        auto &f = pp.free[i];
+        if (std::get<0>(f) == c->device && std::get<1>(f) == fl && std::get<2>(f) >= b) {
+            c->d_peer = static_cast<double *>(std::get<3>(f));
+            pp.free.erase(pp.free.begin() + (long)i);
+            return HMMBW_OK;
+        }
+    }
+    void *p = nullptr;
+    HIP_TRY(hipExtMallocWithFlags(&p, b, fl));
+    pp.owned[p] = std::make_tuple(c->device, fl, b);
+    c->d_peer = static_cast<double *>(p);
+    return HMMBW_OK;
+}
+
+void peer_region_free(hmmbw_ctx *c) {
+    if (!c->d_peer) return;
+    PeerPool &pp = peer_pool();
+    {
+        std::lock_guard<std::mutex> lk(pp.mu);
+        auto it = pp.owned.find(c->d_peer);
+        if (it != pp.owned.end()) {
+            pp.free.emplace_back(std::get<0>(it->second), std::get<1>(it->second), std::get<2>(it->second), c->d_peer);
+            c->d_peer = nullptr;
+            return;
+        }
+    }
+    (void)hipFree(c->d_peer);
+    c->d_peer = nullptr;
+}
+
+// message of a device-side stop (IterState::error, set with done by a bounded wait that expired)
+std::string device_error(const IterState &h) {
+    if (h.error_src == kErrWorkQueue)
+        return "EM stopped on a device-side failure: a wide work-queue backward sweep did not see its tile's "
+               "forward sweep finish within HMMBW_OPT_WQ_TIMEOUT_MS";
+    return "EM stopped on a device-side failure: a rank did not deliver its statistics to the peer all-reduce "
+           "within HMMBW_OPT_PEER_TIMEOUT_MS";
+}
+
 }  // namespace
 
 extern "C" {
@@ -997,6 +1101,7 @@ int hmmbw_ctx_create(int device, int n_states, int n_symbols, hmmbw_ctx **out) {
     c->NP = c->wide ? 16 * ((n_states + 15) / 16) : 0;
     c->G = c->wide ? c->NP : (n_states <= 2 ? 2 : n_states <= 4 ? 4 : n_states <= 8 ? 8 : 16);
     c->U = c->wide ? 16 : kWave / c->G;
+    if (const char *we = std::getenv("HMMBW_WIDE_WQ")) c->wq_mode = std::atoi(we) == 0 ? 0 : (std::atoi(we) == 1 ? 1 : -1);
     int rc = set_device(c);
     if (!rc) {
         int khz = 0;
@@ -1051,8 +1156,7 @@ int hmmbw_ctx_destroy(hmmbw_ctx *c) {
         c->comm = nullptr;
     }
     peer_detach(c);
-    if (c->d_peer) (void)hipFree(c->d_peer);  // its own allocation (IPC-exported), not the block cache
-    c->d_peer = nullptr;
+    peer_region_free(c);
     dfree(c->d_xsum);
     free_obs(c);
     for (auto e : c->ev_free) (void)hipEventDestroy(e);
@@ -1275,27 +1379,6 @@ int hmmbw_set_observations(hmmbw_ctx *c, const int64_t *offsets, const int32_t *
     }
     if (!rc) rc = dalloc(&c->d_logp, (size_t)std::max<int64_t>(R, 1));
     if (!rc) rc = dalloc(&c->d_llpart, 4 * (size_t)std::max(nblocks, 1LL));
-    // Wide path with many tiles per CU: a workgroup per forward and per backward sweep, taken from a queue
-    // in dispatch order (k_estep_mfma<..., WQ>), so the CUs' loads even out in sweeps instead of whole
-    // tiles.  Measured (round 4): whole cfg5 (3,125 tiles) 12.06 against 12.37 ms per iteration; the cfg5
-    // shard (391 tiles, 1.5 per CU) 2.17 against 1.85 ms: with so few tiles per CU the backward sweeps
-    // (0.63 of a tile) start late and form the tail, so the queue is used from 4 tiles per CU.
-    // HMMBW_WIDE_WQ=0 / 1 turns it off / on whenever there are more tiles than CUs.
-    long long wq_grid = 0;
-    if (!rc && c->wide && !c->det) {
-        int ncu = 0;
-        (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device);
-        const char *we = std::getenv("HMMBW_WIDE_WQ");
-        const long long from = (we && std::atoi(we) == 1) ? ncu : 4LL * ncu;
-        if (ncu > 0 && nblocks > from && !(we && std::atoi(we) == 0) && nblocks < (1LL << 30)) {
-            wq_grid = 2 * nblocks;
-            rc = dalloc(&c->d_wq, (size_t)nblocks + 2);
-            if (!rc) {
-                const hipError_t e = hipMemset(c->d_wq, 0, sizeof(unsigned) * ((size_t)nblocks + 2));
-                if (e != hipSuccess) return fail(HMMBW_E_HIP, std::string("hipMemset: ") + hipGetErrorString(e));
-            }
-        }
-    }
     if (rc) return rc;
     HIP_TRY(hipMemcpy(c->d_sym, hsym.data(), sizeof(uint16_t) * hsym.size(), hipMemcpyHostToDevice));
     if (c->wide || c->det) {
@@ -1320,9 +1403,9 @@ int hmmbw_set_observations(hmmbw_ctx *c, const int64_t *offsets, const int32_t *
     c->nblocks = nblocks;
     c->nfull = nfull;
     c->xact = xact;
-    c->wq_grid = wq_grid;
     if (const char *pe = std::getenv("HMMBW_PRIO")) c->prio = std::atoi(pe);
     c->has_obs = true;
+    if (int rc2 = ensure_wq(c)) return rc2;
     return ensure_zf(c);
 }
 
@@ -1385,11 +1468,46 @@ int hmmbw_set_option(hmmbw_ctx *c, int key, int64_t value) {
             ((unsigned long long)c->live_epoch << 32) | (unsigned long long)(unsigned)h.iteration;
         return HMMBW_OK;
     }
+    if (key == HMMBW_OPT_WQ_TIMEOUT_MS) {
+        if (value < 0) return fail(HMMBW_E_INVALID, "work-queue timeout must be >= 0 ms");
+        c->wq_timeout_ms = value;
+        return HMMBW_OK;
+    }
+    if (key == HMMBW_OPT_WIDE_WQ) {
+        if (value < -1 || value > 1) return fail(HMMBW_E_INVALID, "HMMBW_OPT_WIDE_WQ: -1 (auto), 0 (off) or 1 (on)");
+        if (int rc = set_device(c)) return rc;
+        c->wq_mode = (int)value;
+        return ensure_wq(c);
+    }
     if (key == HMMBW_OPT_ABLATE) {  // diagnostics: results are wrong while set
         c->ablate = (int)value;
         return HMMBW_OK;
     }
     return fail(HMMBW_E_INVALID, "unknown option " + std::to_string(key));
+}
+
+int hmmbw_get_option(const hmmbw_ctx *c, int key, int64_t *value) {
+    if (!c || !value) return fail(HMMBW_E_INVALID, "null argument");
+    switch (key) {
+        case HMMBW_OPT_SAFE_SCALING: *value = c->force_safe; return HMMBW_OK;
+        case HMMBW_OPT_ABLATE: *value = c->ablate; return HMMBW_OK;
+        case HMMBW_OPT_STAT_COPIES: *value = c->ncopies; return HMMBW_OK;
+        case HMMBW_OPT_MERGE_MSTEP: *value = c->merge_mstep ? 1 : 0; return HMMBW_OK;
+        case HMMBW_OPT_DETERMINISTIC: *value = c->det ? 1 : 0; return HMMBW_OK;
+        case HMMBW_OPT_ALLREDUCE: *value = c->ar_kind; return HMMBW_OK;
+        case HMMBW_OPT_PEER_TIMEOUT_MS: *value = c->peer_timeout_ms; return HMMBW_OK;
+        case HMMBW_OPT_LIVE_STATUS: *value = c->h_live ? 1 : 0; return HMMBW_OK;
+        case HMMBW_OPT_WQ_TIMEOUT_MS: *value = c->wq_timeout_ms; return HMMBW_OK;
+        case HMMBW_OPT_WIDE_WQ: *value = c->wq_mode; return HMMBW_OK;
+        case HMMBW_INFO_WIDE_WQ_ACTIVE: *value = c->d_wq ? 1 : 0; return HMMBW_OK;
+        case HMMBW_INFO_WAVES: *value = c->wide ? c->nblocks * (c->NP / 16) : c->nwaves; return HMMBW_OK;
+        case HMMBW_INFO_WORKGROUPS: *value = c->d_wq ? c->wq_grid : c->nblocks; return HMMBW_OK;
+        case HMMBW_INFO_WAVES_PER_WORKGROUP: *value = c->wide ? c->NP / 16 : kBlock / kWave; return HMMBW_OK;
+        case HMMBW_INFO_FULL_WORKGROUPS: *value = c->wide ? c->nblocks : std::min(c->nfull, c->nblocks); return HMMBW_OK;
+        case HMMBW_INFO_EXTRA_WAVES: *value = c->wide ? 0 : c->xact; return HMMBW_OK;
+        case HMMBW_INFO_PEER_CHUNKS: *value = c->d_peer ? c->peer_nch : 0; return HMMBW_OK;
+        default: return fail(HMMBW_E_INVALID, "unknown option " + std::to_string(key));
+    }
 }
 
 int hmmbw_set_params(hmmbw_ctx *c, const double *pi, const double *A, const double *B) {
@@ -1430,6 +1548,9 @@ int hmmbw_reset_training(hmmbw_ctx *c, double epsilon, int64_t max_iterations) {
     ++c->live_epoch;  // the mirror's records of the previous run no longer count (hmmbw_status_live_wait)
     HIP_TRY(hipMemsetAsync(c->d_copies, 0, sizeof(double) * 3 * c->ncopies * c->copy_len(), c->stream));
     if (c->d_xbuf) HIP_TRY(hipMemsetAsync(c->d_xbuf, 0, sizeof(double) * 3 * (size_t)c->xlen, c->stream));
+    // the work queue's counters and flags: a run stopped by a work-queue timeout leaves them armed (the
+    // workgroups that start after the stop return at once and never reach the re-arm)
+    if (c->d_wq) HIP_TRY(hipMemsetAsync(c->d_wq, 0, sizeof(unsigned) * ((size_t)c->nblocks + 2), c->stream));
     c->e_count = 0;
     c->armed = true;
     return HMMBW_OK;
@@ -1645,10 +1766,9 @@ int hmmbw_peer_region(hmmbw_ctx *c, void **region, int64_t *bytes) {
     if (!c->d_peer || c->peer_n != n || c->peer_world != c->world) {
         peer_detach(c);
         HIP_TRY(hipDeviceSynchronize());
-        if (c->d_peer) HIP_TRY(hipFree(c->d_peer));
-        c->d_peer = nullptr;
+        peer_region_free(c);
         // its own allocation (exported with hipIpcGetMemHandle), never a block of the cache
-        HIP_TRY(hipMalloc(reinterpret_cast<void **>(&c->d_peer), b));
+        if (int rc = peer_region_alloc(c, b)) return rc;
         HIP_TRY(hipMemset(c->d_peer, 0, b));
         dfree(c->d_xsum);
         if (int rc = dalloc(&c->d_xsum, (size_t)slot)) return rc;
@@ -1839,8 +1959,7 @@ int hmmbw_get_status(hmmbw_ctx *c, hmmbw_status *st, hmmbw_iter_record *rec, int
         HIP_TRY(hipMemcpyAsync(hist.data(), c->d_hist, sizeof(double) * hist.size(), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     fill_status(h, st);
-    if (h.error) return fail(h.error, "EM stopped on a device-side failure: a rank did not deliver its statistics to "
-                                      "the peer all-reduce within HMMBW_OPT_PEER_TIMEOUT_MS");
+    if (h.error) return fail(h.error, device_error(h));
     if (rec && count > 0) {
         if (first < 0 || first + count > h.iteration || first < h.iteration - kHist)
             return fail(HMMBW_E_INVALID, "requested iteration records are not available");
@@ -1888,8 +2007,7 @@ int hmmbw_status_wait(hmmbw_ctx *c, int64_t ticket, hmmbw_status *st, hmmbw_iter
     HIP_TRY(hipEventSynchronize(sn.ev));  // this snapshot only, not the work enqueued after it
     const IterState h = *sn.st;
     fill_status(h, st);
-    if (h.error) return fail(h.error, "EM stopped on a device-side failure: a rank did not deliver its statistics to "
-                                      "the peer all-reduce within HMMBW_OPT_PEER_TIMEOUT_MS");
+    if (h.error) return fail(h.error, device_error(h));
     if (rec && count > 0) {
         if (first < sn.first || first + count > h.iteration || first + count > sn.first + kHist ||
             first < h.iteration - kHist)  // overwritten in the ring before the snapshot was taken
@@ -1952,8 +2070,7 @@ int hmmbw_status_live_wait(hmmbw_ctx *c, int64_t iterations, hmmbw_status *st, h
         }
     }
     fill_status(h, st);
-    if (h.error) return fail(h.error, "EM stopped on a device-side failure: a rank did not deliver its statistics to "
-                                      "the peer all-reduce within HMMBW_OPT_PEER_TIMEOUT_MS");
+    if (h.error) return fail(h.error, device_error(h));
     if (rec && count > 0) {
         if (first < 0 || first + count > h.iteration || first < h.iteration - kHist)
             return fail(HMMBW_E_INVALID, "requested iteration records are not available");

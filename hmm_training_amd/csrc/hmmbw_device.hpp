@@ -86,9 +86,11 @@ struct IterState {
     long long max_iterations;
     int done;
     int converged;
-    int error;  // HMMBW_E_* of a device-side failure (peer all-reduce timeout); done is set with it
-    int pad_;
+    int error;      // HMMBW_E_* of a device-side failure; done is set with it
+    int error_src;  // which bounded wait failed: kErrPeer (peer all-reduce) or kErrWorkQueue (wide work queue)
 };
+constexpr int kErrPeer = 1;
+constexpr int kErrWorkQueue = 2;
 
 // Observation layout in HBM (built once by hmmbw_set_observations).
 //   slot = wave * U + u  ->  caller sequence slot_seq[slot] (-1: padding), length slot_len[slot]
@@ -179,6 +181,7 @@ struct EArgs {
     unsigned *wq;
     unsigned *wq_flag;
     int wq_units;  // tiles
+    long long wq_timeout_ticks;  // bound (wall-clock ticks) of a backward unit's wait for its forward
 };
 
 // Grouped launch (k_estep_small_group): per-model arguments and first workgroups (start[nm] = grid)
@@ -525,9 +528,14 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
 
     if (wactive && wave < a.L.nwaves) {
         const long long slot = wave * U + u;
+#ifdef HMMBW_DIAG_XHALF  // diagnostics (timing only, results wrong): the spread map's extra waves run half their steps
+        const int Tw = xblk ? max(kChunk, (a.L.wave_T[wave] / 2) & ~(kChunk - 1)) : a.L.wave_T[wave];
+        const int T = min(a.L.slot_len[slot], Tw);
+#else
         const int T = a.L.slot_len[slot];
-        const int seq = a.L.slot_seq[slot];
         const int Tw = a.L.wave_T[wave];
+#endif
+        const int seq = a.L.slot_seq[slot];
         const bool full = a.L.wave_full[wave] != 0;
         const int nch = (Tw + kChunk - 1) / kChunk;
         const long long symbase = a.L.wave_symoff[wave] + u * kChunk;  // pack index of this slot's chunk-0 entry
@@ -1274,6 +1282,7 @@ __device__ bool record_iteration(const MArgs &m, const IterState &in, double L) 
         sys(&sl->done, o.done);
         sys(&sl->converged, o.converged);
         sys(&sl->error, o.error);
+        sys(&sl->error_src, o.error_src);
         __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): every store above is acknowledged
         sys(&m.live->pub, ((unsigned long long)m.live_epoch << 32) | (unsigned long long)(unsigned)o.iteration);
     }
@@ -1603,6 +1612,7 @@ __device__ bool merged_mstep(const EArgs &a, double *sP, double *sH, double *sPA
         in.done = m.state->done;
         in.converged = m.state->converged;
         in.error = m.state->error;
+        in.error_src = m.state->error_src;
         in.last_L = m.state->last_L;
         in.last_diff = m.state->last_diff;
     }

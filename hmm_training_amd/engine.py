@@ -25,9 +25,9 @@ from typing import Callable, List, Optional, Sequence, Tuple
 import numpy as np
 import torch
 
-from ._lib import (ALLREDUCE, OPT_ALLREDUCE, OPT_DETERMINISTIC, OPT_LIVE_STATUS, OPT_MERGE_MSTEP, OPT_PEER_TIMEOUT_MS,
-                   OPT_SAFE_SCALING,
-                   OPT_STAT_COPIES, TOPOLOGY, TOPOLOGY_NAME, IterRecord, Status, check, lib)
+from ._lib import (ALLREDUCE, INFO_WIDE_WQ_ACTIVE, OPT_ALLREDUCE, OPT_DETERMINISTIC, OPT_LIVE_STATUS, OPT_MERGE_MSTEP,
+                   OPT_PEER_TIMEOUT_MS, OPT_SAFE_SCALING, OPT_STAT_COPIES, OPT_WIDE_WQ, OPT_WQ_TIMEOUT_MS, TOPOLOGY,
+                   TOPOLOGY_NAME, IterRecord, Status, check, lib)
 
 IterCallback = Callable[[int, float, float], None]
 
@@ -260,6 +260,41 @@ class BaumWelchEngine:
     @property
     def native_comm(self) -> bool:
         return self._native
+
+    def set_option(self, key: int, value: int) -> None:
+        check(self._lib.hmmbw_set_option(self._ctx, int(key), int(value)))
+
+    def get_option(self, key: int) -> int:
+        v = ctypes.c_int64()
+        check(self._lib.hmmbw_get_option(self._ctx, int(key), ctypes.byref(v)))
+        return v.value
+
+    def set_work_queue(self, mode: int, timeout_ms: Optional[int] = None) -> None:
+        """Wide path (16 < N <= 64): HMMBW_OPT_WIDE_WQ (-1 auto from 4 tiles per CU, 0 off, 1 on when the
+        tiles exceed the CUs) and the bound of its device-side wait (HMMBW_OPT_WQ_TIMEOUT_MS)."""
+        self.set_option(OPT_WIDE_WQ, mode)
+        if timeout_ms is not None:
+            self.set_option(OPT_WQ_TIMEOUT_MS, timeout_ms)
+
+    def launch_map(self) -> dict:
+        """The E-step launch's wave map (HMMBW_INFO_*): active waves, workgroups, waves per workgroup, the
+        workgroups with every wave active and the active waves of each workgroup after them."""
+        from ._lib import (INFO_EXTRA_WAVES, INFO_FULL_WORKGROUPS, INFO_WAVES, INFO_WAVES_PER_WORKGROUP,
+                           INFO_WORKGROUPS)
+        return {"waves": self.get_option(INFO_WAVES), "workgroups": self.get_option(INFO_WORKGROUPS),
+                "waves_per_workgroup": self.get_option(INFO_WAVES_PER_WORKGROUP),
+                "full_workgroups": self.get_option(INFO_FULL_WORKGROUPS),
+                "extra_waves": self.get_option(INFO_EXTRA_WAVES), "work_queue": self.work_queue_active}
+
+    def peer_chunks(self) -> int:
+        """Chunks of the peer all-reduce payload (one flag per (rank, chunk) per iteration), 0 without a region."""
+        from ._lib import INFO_PEER_CHUNKS
+        return self.get_option(INFO_PEER_CHUNKS)
+
+    @property
+    def work_queue_active(self) -> bool:
+        """True if the loaded observations' E-step runs on the wide work queue (HMMBW_INFO_WIDE_WQ_ACTIVE)."""
+        return self.get_option(INFO_WIDE_WQ_ACTIVE) == 1
 
     def set_params(self, pi: np.ndarray, A: np.ndarray, B: np.ndarray) -> None:
         pi = np.ascontiguousarray(pi, dtype=np.float64).reshape(self.N)
@@ -506,12 +541,26 @@ class BaumWelchEngine:
         return 8 * n.value
 
     def close(self) -> None:
+        """Destroy the context.  With the peer all-reduce set up, every rank must call close() at the same
+        point (a collective): the ranks first meet at a barrier, so no rank frees its IPC-exported receive
+        region while another may still push into it (a rank whose wait timed out, or bench's fallback
+        after a failed leg)."""
         if getattr(self, "_ctx", None):
+            if getattr(self, "_peer_ok", False) and self.world_size > 1:
+                try:
+                    import torch.distributed as dist
+                    if dist.is_available() and dist.is_initialized():
+                        torch.cuda.synchronize(self.device)  # this rank's pushes have landed
+                        dist.barrier(group=self._group)       # ... and every other rank's too
+                except Exception:  # noqa: BLE001 - a broken process group must not keep the context alive
+                    pass
             self._lib.hmmbw_ctx_destroy(self._ctx)
             self._ctx = None
 
     def __del__(self):
         try:
+            if getattr(self, "_ctx", None):  # garbage collection is no collective: skip the barrier
+                self._peer_ok = False
             self.close()
         except Exception:
             pass

@@ -32,9 +32,10 @@
 extern "C" {
 #endif
 
-#define HMMBW_ABI_VERSION 4 /* 2: hmmbw_iterate_begin/_end, status snapshots, comm info/payload;
+#define HMMBW_ABI_VERSION 5 /* 2: hmmbw_iterate_begin/_end, status snapshots, comm info/payload;
                               3: peer all-reduce (hmmbw_peer_*), HMMBW_E_TIMEOUT, cache trim, split timing;
-                              4: live status mirror (HMMBW_OPT_LIVE_STATUS, hmmbw_status_live_wait) */
+                              4: live status mirror (HMMBW_OPT_LIVE_STATUS, hmmbw_status_live_wait);
+                              5: hmmbw_get_option, HMMBW_OPT_WQ_TIMEOUT_MS, HMMBW_OPT_WIDE_WQ */
 
 #define HMMBW_OK 0
 #define HMMBW_E_INVALID (-1)        /* bad argument (shape, range, null pointer)             */
@@ -44,8 +45,10 @@ extern "C" {
 #define HMMBW_E_EMPTY_SEQUENCE (-5) /* a sequence of length 0: the reference raises IndexError
                                        at hmm_training.py:376 / hmm_testing.py:75              */
 #define HMMBW_E_SYMBOL_RANGE (-6)   /* symbol id >= M: numpy IndexError at hmm_training.py:360 */
-#define HMMBW_E_TIMEOUT (-7)        /* a rank did not deliver its statistics to the peer all-reduce in time
-                                       (bounded device-side wait; EM stops, status calls report it)  */
+#define HMMBW_E_TIMEOUT (-7)        /* a bounded device-side wait expired: a rank did not deliver its
+                                       statistics to the peer all-reduce in time, or a wide work-queue
+                                       backward sweep did not see its forward finish (EM stops, the
+                                       status calls report it; hmmbw_last_error says which)           */
 
 /* Transition-matrix kernel variant (the reference skips -inf transitions,
  * hmm_training.py:143-144,186-188; a left-to-right A keeps its zero pattern under EM). */
@@ -234,7 +237,7 @@ int hmmbw_score(hmmbw_ctx *ctx, double *out);
  * form when magnitudes leave [2^-900, 2^900]).  Results agree to fp64 rounding either way. */
 #define HMMBW_OPT_SAFE_SCALING 1
 /* Diagnostics only (profiling ablations; results are WRONG while nonzero): bit 0 skips the E-step's
- * statistics flush, bit 1 skips its backward sweep. */
+ * statistics flush, bit 1 skips its backward sweep, bit 2 skips the separate (unmerged) M-step kernel. */
 #define HMMBW_OPT_ABLATE 2
 /* Number of statistics accumulator copies the E-step's workgroups spread their atomics over
  * (workgroup b adds into copy b % n; default 2). */
@@ -262,7 +265,38 @@ int hmmbw_score(hmmbw_ctx *ctx, double *out);
 /* 1: keep a host mirror of the convergence state that the M-steps update (hmmbw_status_live_wait);
  * 0 (default): off.  Synchronises the context stream when changed. */
 #define HMMBW_OPT_LIVE_STATUS 10
+/* Bound, in milliseconds, of the wide work queue's device-side wait (16 < N <= 64 with many tiles per CU,
+ * HMMBW_OPT_WIDE_WQ): a backward sweep waits for its tile's forward sweep, which runs on a resident
+ * workgroup, so the wait always ends; past the bound the iteration fails with HMMBW_E_TIMEOUT (EM stops,
+ * the sweep's statistics are not added) instead of reading alpha_hat that may not be there.  Default
+ * 10000; 0 expires at once (tests the error path). */
+#define HMMBW_OPT_WQ_TIMEOUT_MS 11
+/* Wide E-step work queue (a workgroup per forward and per backward sweep of each 16-sequence tile, taken
+ * in dispatch order, so the CUs' loads even out in sweeps instead of whole tiles): -1 (default) when the
+ * tiles exceed 4 per CU, 1 whenever they exceed the CU count, 0 never.  The environment variable
+ * HMMBW_WIDE_WQ=0/1 sets a new context's default.  Takes effect at once. */
+#define HMMBW_OPT_WIDE_WQ 12
 int hmmbw_set_option(hmmbw_ctx *ctx, int key, int64_t value);
+/* The current value of an option above, or a read-only fact about the loaded observations' E-step launch:
+ * HMMBW_INFO_WIDE_WQ_ACTIVE    1 if it runs on the wide work queue;
+ * HMMBW_INFO_WAVES             active waves (small kernels: sequence-group waves; wide: tiles x NP/16);
+ * HMMBW_INFO_WORKGROUPS        workgroups of the launch;
+ * HMMBW_INFO_WAVES_PER_WORKGROUP  waves per workgroup;
+ * HMMBW_INFO_FULL_WORKGROUPS   workgroups with every wave active (small kernels: the spread map puts the
+ *                              waves past one per SIMD into workgroups of HMMBW_INFO_EXTRA_WAVES active waves
+ *                              after these);
+ * HMMBW_INFO_EXTRA_WAVES       active waves of each workgroup after the full ones;
+ * HMMBW_INFO_PEER_CHUNKS       chunks of the peer all-reduce payload (each rank writes and polls one flag
+ *                              per (rank, chunk) per iteration), 0 without a peer region.
+ * (bench.py's roofline bounds price the busiest CU and SIMD from this map.) */
+#define HMMBW_INFO_WIDE_WQ_ACTIVE 101
+#define HMMBW_INFO_WAVES 102
+#define HMMBW_INFO_WORKGROUPS 103
+#define HMMBW_INFO_WAVES_PER_WORKGROUP 104
+#define HMMBW_INFO_FULL_WORKGROUPS 105
+#define HMMBW_INFO_EXTRA_WAVES 106
+#define HMMBW_INFO_PEER_CHUNKS 107
+int hmmbw_get_option(const hmmbw_ctx *ctx, int key, int64_t *value);
 
 /* E-step kernel timing with HIP events on the context stream (for bench/roofline).  Returns the
  * accumulated time and count of the timed launches so far, then (enable >= 0) resets and sets the

@@ -68,12 +68,19 @@ def test_bench_single_gpu_line():
         assert k in d, k
     assert d["n_gpus"] == 1 and d["steps"] == 10 and d["value"] > 0
     rf = d["roofline"]
-    # the binding ceiling of the launch: every bound is achieved / peak of one resource, so frac <= 1;
-    # the survey's byte model stays beside it (effective_bw_frac, not a bound: it can exceed 1)
-    assert rf["bound"] == rf["bounds"]["binding"] in ("hbm", "valu", "simd_valu", "cu_lds")
-    assert 0 < rf["frac"] <= 1.0 and rf["frac"] == max(b["frac"] for b in rf["bounds"].values() if isinstance(b, dict))
-    assert rf["effective_bw_frac"] > 0 and rf["bounds"]["waves_on_busiest_simd"] >= 1
-    assert d["cpu_baseline"]["value"] > 0
+    # algorithmic bytes per launch (24T + 16NT + 8 per sequence) over the launch time vs 8 TB/s
+    assert rf["bound"] == "hbm" and rf["unit"] == "GB/s" and rf["peak"] == 8000.0
+    assert rf["achieved"] == pytest.approx((24 * 200 + 16 * 8 * 200 + 8) * 10_000 / (rf["kernel_ms"] * 1e-3) / 1e9)
+    assert rf["frac"] == pytest.approx(rf["achieved"] / rf["peak"])
+    # the tightest ceiling the counters measure: achieved / peak of one resource, so <= 1, with provenance
+    bd = rf["bounds"]
+    assert rf["binding"]["resource"] == bd["binding"] in ("hbm", "valu", "simd_valu", "cu_lds")
+    assert 0 < rf["binding"]["frac"] <= 1.0
+    assert rf["binding"]["frac"] == max(b["frac"] for b in bd.values() if isinstance(b, dict) and "frac" in b)
+    # the busiest SIMD and CU on the engine's spread map: cfg3's 1,250 waves = 256 full workgroups + 113 of 2
+    assert rf["launch_map"]["waves"] == 1250 and rf["launch_map"]["extra_waves"] == 2
+    assert bd["waves_on_busiest_simd"] == 2 and bd["waves_on_busiest_cu"] == 6
+    assert rf["kernel_src_sha16"] and d["cpu_baseline"]["value"] > 0
 
 
 @pytest.mark.gpu
@@ -115,3 +122,18 @@ def test_bench_skewed_symbols_line():
     assert r.returncode == 0, r.stderr[-3000:]
     d = _json_line(r.stdout)
     assert d["config"]["symbols"] == "H" and d["value"] > 0
+
+
+def test_engine_waves_on_the_spread_map():
+    """The busiest SIMD and CU of the roofline bounds, counted on the engine's launch map (HMMBW_INFO_*):
+    cfg3's 1,250 waves = 256 full workgroups + 113 of 2 active waves -> 6 waves on the busiest CU, 2 on its
+    busiest SIMD; the cfg4 shard (1,563 waves, no spread) = 391 full workgroups -> 8 and 2."""
+    sys.path.insert(0, ROOT)
+    import bench
+    cfg3 = {"waves": 1250, "workgroups": 369, "waves_per_workgroup": 4, "full_workgroups": 256, "extra_waves": 2,
+            "work_queue": False}
+    assert bench.engine_waves(10_000, 8, cfg3) == (1250, 2, 6)
+    cfg4 = {"waves": 1563, "workgroups": 391, "waves_per_workgroup": 4, "full_workgroups": 391, "extra_waves": 4,
+            "work_queue": False}
+    assert bench.engine_waves(12_500, 8, cfg4) == (1563, 2, 8)
+    assert bench.engine_waves(10_000, 8) == (1250, 2, 5)  # no map: pigeonhole

@@ -100,7 +100,7 @@ def statistics_pass(eng, N, K, R):
     return g, ll, eng.params(normalise=False)
 
 
-def run_vs_oracle(oracle, R, T, N, K, topology, iters, seed, symbols="U", deterministic=False):
+def run_vs_oracle(oracle, R, T, N, K, topology, iters, seed, symbols="U", deterministic=False, work_queue=None):
     from hmm_training_amd.engine import BaumWelchEngine, StatsLayout
     sym = _symbols(R, T, N, K, symbols, seed)
     off = np.arange(R + 1, dtype=np.int64) * T
@@ -112,6 +112,8 @@ def run_vs_oracle(oracle, R, T, N, K, topology, iters, seed, symbols="U", determ
         eng.set_observations(offsets=off, symbols=sym)
         eng.set_params(pi, A, B)
         assert eng.topology == topology
+        if work_queue is not None:  # which wide E-step form the library chose on its own (no option set)
+            assert eng.work_queue_active == work_queue
         # -------- production iterations, enqueued together (merged M-steps) --------
         eng.reset(0.0, iters)
         eng.enqueue_iterations(iters)
@@ -169,6 +171,28 @@ def test_cfg5_full_shape_slice_vs_oracle(oracle_mt):
 def test_cfg5_shard_full_size_vs_oracle(oracle_mt):
     """BASELINE cfg5's per-GPU shard: 6,250 x T=400, N=64, K=1024, dense, 2 EM iterations vs the oracle."""
     run_vs_oracle(oracle_mt, 6_250, 400, 64, 1024, "dense", 2, seed=5)
+
+
+def test_wide_work_queue_one_context_full_size_vs_oracle(oracle_mt):
+    """The wide work queue (a workgroup per forward and per backward sweep, estep_mfma.hpp WQ) as the
+    library selects it on its own: ONE context above the 4-tiles-per-CU threshold (18,000 x T=200 = 1,125
+    tiles, N=64, K=256, dense), 2 EM iterations and a statistics pass against the oracle
+    (hmm_training.py:351-514), including the counter and flag re-arm by the last of 2,250 workgroups."""
+    import torch
+    ncu = torch.cuda.get_device_properties(0).multi_processor_count
+    R = 18_000
+    assert (R + 15) // 16 > 4 * ncu, "the case must sit above the work queue's threshold"
+    run_vs_oracle(oracle_mt, R, 200, 64, 256, "dense", 2, seed=18, work_queue=True)
+
+
+def test_cfg5_shard_is_not_on_the_work_queue(oracle_mt):
+    """The cfg5 per-GPU shard (391 tiles, 1.5 per CU) keeps one workgroup per tile: the queue measured
+    slower there (profiles/r4/wide_work_queue_ab.txt)."""
+    from hmm_training_amd.engine import BaumWelchEngine
+    with BaumWelchEngine(64, 1024, topology="dense") as eng:
+        eng.set_observations(offsets=np.arange(6_251, dtype=np.int64) * 400,
+                             symbols=np.zeros(6_250 * 400, dtype=np.int32))
+        assert not eng.work_queue_active
 
 
 def test_cfg3_full_size_deterministic_vs_oracle(oracle_mt):

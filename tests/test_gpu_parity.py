@@ -180,10 +180,48 @@ def test_wide_work_queue_vs_oracle(N, equal, wq, oracle, monkeypatch):
     with BaumWelchEngine(N, K, topology="dense") as eng:
         eng.set_observations(obs)
         eng.set_params(pi, A, B)
+        assert eng.work_queue_active == (wq == "1")
         trace = []
         eng.train(1e-9, 3, lambda k, L, df: trace.append(L))
         assert_ll(trace, ref.trace_L)
         assert_ll(eng.loglik(), ref.logP)
+        p2, A2, B2 = eng.params(normalise=True)
+    assert_params(A2, ref.A, "A")
+    assert_params(B2, ref.B, "B")
+    assert_params(p2, ref.pi, "pi")
+
+
+def test_wide_work_queue_timeout_is_an_error(oracle):
+    """The work queue's bounded wait (estep_mfma.hpp): a backward sweep whose forward has not finished
+    within HMMBW_OPT_WQ_TIMEOUT_MS stops EM with HMMBW_E_TIMEOUT, reported by the status calls, instead of
+    reading alpha_hat that may not be there.  A 0-ms bound expires before the first look at the flag, so
+    the first iteration fails; the next run (reset re-arms the queue) with the default bound then matches
+    the oracle (hmm_training.py:351-514)."""
+    import torch
+    from hmm_training_amd._lib import HMMBW_E_TIMEOUT, HMMBWError
+    from hmm_training_amd.engine import BaumWelchEngine, to_csr
+    ncu = torch.cuda.get_device_properties(0).multi_processor_count
+    N, K, R = 32, 64, 16 * ncu + 16 * 9 + 3
+    rng = np.random.default_rng(77)
+    obs, pi, A, B = random_problem(rng, N, K, R=R, tmax=24, topology="dense")
+    off, sym = to_csr(obs)
+    ref = oracle.hmm_training(off, sym.astype(np.int64), N, K, 1e-9, 2, pi, A, B)
+    with BaumWelchEngine(N, K, topology="dense") as eng:
+        eng.set_observations(obs)
+        eng.set_params(pi, A, B)
+        eng.set_work_queue(1, timeout_ms=0)
+        assert eng.work_queue_active
+        eng.reset(1e-9, 2)
+        eng.enqueue_iterations(2)
+        with pytest.raises(HMMBWError) as ei:
+            eng.status()
+        assert ei.value.code == HMMBW_E_TIMEOUT
+        assert "work-queue" in str(ei.value)
+        eng.set_params(pi, A, B)
+        eng.set_work_queue(1, timeout_ms=10000)
+        trace = []
+        eng.train(1e-9, 2, lambda k, L, df: trace.append(L))
+        assert_ll(trace, ref.trace_L)
         p2, A2, B2 = eng.params(normalise=True)
     assert_params(A2, ref.A, "A")
     assert_params(B2, ref.B, "B")

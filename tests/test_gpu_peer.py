@@ -10,7 +10,7 @@ On one GPU:
   push that is queued behind it), against the reference's fixtures and the oracle;
 * one rank through the native hmmbw_iterate loop (push to itself, wait, sum);
 * the bounded wait: a rank whose peer never pushes stops with HMMBW_E_TIMEOUT instead of spinning;
-* two PROCESSES on the same GPU, IPC handles exchanged over a gloo process group (the path an 8-GPU run
+* two and four PROCESSES on the same GPU, IPC handles exchanged over a gloo process group (the path an 8-GPU run
   takes, minus xGMI), each rank ending on the oracle's parameters.
 """
 import ctypes
@@ -269,16 +269,24 @@ dist.destroy_process_group()
 """
 
 
-def test_peer_allreduce_two_processes_ipc(oracle_mt, tmp_path):
-    """Two rank processes on cuda:0: the IPC handles go through a gloo process group (all_gather_object),
-    each rank maps the other's region with hipIpcOpenMemHandle, and the engine's train() runs the native
-    peer loop.  Both ranks must end on the oracle's L trace and parameters."""
+@pytest.mark.parametrize("world,N,K,topology", [(2, 8, 256, "left_to_right"), (4, 8, 256, "left_to_right"),
+                                                 (4, 24, 64, "dense")])
+def test_peer_allreduce_processes_ipc(oracle_mt, tmp_path, world, N, K, topology):
+    """`world` rank processes on cuda:0: the IPC handles go through a gloo process group
+    (all_gather_object), each rank maps every other rank's region with hipIpcOpenMemHandle (not
+    hmmbw_peer_attach), and the engine's train() runs the native peer loop (one k_peer_allreduce per EM
+    iteration: world x chunks pushes, each rank's flags polled and its slots summed in rank order).  Every
+    rank must end on the oracle's L trace and parameters (hmm_training.py:351-514) with bitwise-identical
+    traces; world 4 covers the per-peer slot and flag layout beyond a pair, N = 24 the wide path's payload."""
     from hmm_training_amd.hmm_training import default_initial_params
-    rng = np.random.default_rng(41)
-    N, K, R, iters = 8, 256, 600, 4
+    rng = np.random.default_rng(41 + world + N)
+    R, iters = 600, 4
     obs = [rng.integers(0, K, size=int(t)) for t in rng.integers(40, 200, size=R)]
     pi, A, B = default_initial_params(N, K)
-    case = {"N": N, "K": K, "topology": "left_to_right", "iters": iters, "obs": [o.tolist() for o in obs],
+    if topology == "dense":
+        A = 0.5 * A + 0.5 * rng.dirichlet(np.ones(N), size=N)
+        B = rng.dirichlet(np.full(K, 2.0), size=N)
+    case = {"N": N, "K": K, "topology": topology, "iters": iters, "obs": [o.tolist() for o in obs],
             "pi": pi.tolist(), "A": A.tolist(), "B": B.tolist()}
     cpath, opath = tmp_path / "case.json", tmp_path / "out"
     cpath.write_text(json.dumps(case))
@@ -289,8 +297,8 @@ def test_peer_allreduce_two_processes_ipc(oracle_mt, tmp_path):
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     procs = []
-    for r in range(2):
-        env = dict(os.environ, RANK=str(r), WORLD_SIZE="2", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
                    HMMBW_ROOT=ROOT, HMMBW_CASE=str(cpath), HMMBW_OUT=str(opath))
         procs.append(subprocess.Popen([sys.executable, str(wpath)], env=env))
     try:
@@ -299,14 +307,16 @@ def test_peer_allreduce_two_processes_ipc(oracle_mt, tmp_path):
         for p in procs:
             if p.poll() is None:
                 p.kill()
-    assert rcs == [0, 0], rcs
+    assert rcs == [0] * world, rcs
     off = np.concatenate([[0], np.cumsum([len(o) for o in obs])]).astype(np.int64)
     ref = oracle_mt.hmm_training(off, np.concatenate(obs).astype(np.int64), N, K, 0.0, iters, pi, A, B)
-    outs = [json.load(open(f"{opath}.{r}")) for r in range(2)]
+    outs = [json.load(open(f"{opath}.{r}")) for r in range(world)]
     for r, o in enumerate(outs):
         assert o["iterations"] == iters and o["ar_n"] >= iters
         np.testing.assert_allclose(o["trace"], ref.trace_L, rtol=LL_RTOL)
         assert_params(o["A"], ref.A, f"A rank {r}")
         assert_params(o["B"], ref.B, f"B rank {r}")
         assert_params(o["pi"], ref.pi, f"pi rank {r}")
-    assert outs[0]["trace"] == outs[1]["trace"]
+    for o in outs[1:]:
+        assert o["trace"] == outs[0]["trace"]
+        assert o["A"] == outs[0]["A"] and o["B"] == outs[0]["B"] and o["pi"] == outs[0]["pi"]

@@ -23,7 +23,7 @@ def test_library_exports_every_header_symbol():
     assert set(declared) == set(_lib.EXPORTED), "binding table out of sync with include/hmmbw.h"
     for name in declared:
         assert hasattr(lib, name), name
-    assert lib.hmmbw_abi_version() == _lib.ABI_VERSION == 4
+    assert lib.hmmbw_abi_version() == _lib.ABI_VERSION == 5
 
 
 def test_library_fails_loudly_without_device_or_bad_args():
