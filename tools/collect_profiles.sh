@@ -5,6 +5,8 @@ set -euo pipefail
 TAG=$1; DEST=$2
 SRC=gpurun_out/prof_$TAG
 mkdir -p "profiles/$DEST"
+export HMMBW_PROFILE_SHA=$(cat "$SRC/kernel_src_sha16.txt" 2>/dev/null || true)
+export HMMBW_PROFILE_UTC=$(cat "$SRC/collected_utc.txt" 2>/dev/null || true)
 cp "$SRC/calib_FETCH_SIZE/run_counter_collection.csv" "profiles/$DEST/pmc_calib_FETCH_SIZE.csv"
 cp "$SRC/calib_WRITE_SIZE/run_counter_collection.csv" "profiles/$DEST/pmc_calib_WRITE_SIZE.csv"
 declare -A KEY=([lr_cfg3]=R10000_T200_N8_K256_left_to_right [lrH_cfg3]=R10000_T200_N8_K256_left_to_right_H

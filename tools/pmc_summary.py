@@ -13,9 +13,22 @@ import collections
 import csv
 import glob
 import json
+import time
 import os
 import sys
 
+
+
+def _stamp(d):
+    """Provenance of a summary: UTC collection time and the kernel-source hash of the tree it was collected
+    on (bench.kernel_source_hash), so bench.py can tell a bound from a stale profile."""
+    import sys as _sys
+    _sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    # the profiling run's own record (tools/profile_all.sh writes both on the box), else this tree's
+    d["collected_utc"] = os.environ.get("HMMBW_PROFILE_UTC") or time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime())
+    d["kernel_src_sha16"] = os.environ.get("HMMBW_PROFILE_SHA") or bench.kernel_source_hash()
+    return d
 
 def mean_ns(stats_csv, kern):
     rows = [r for r in csv.DictReader(open(stats_csv)) if kern in r["Name"]]
@@ -52,7 +65,7 @@ def main(src, kernels, config_key=None, kernel_stats=None):
             if ns:
                 d["kernel_ns_trace"] = ns
                 d["clock_ghz"] = d["GRBM_GUI_ACTIVE"] / 8.0 / ns
-        out[kern] = d
+        out[kern] = _stamp(d)
     print(json.dumps(out, indent=2))
 
 

@@ -12,6 +12,9 @@ PART=${2:-all}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
+# provenance of every summary made from this run (tools/collect_profiles.sh stamps them)
+(cd "$R" && python3 -c "import bench; print(bench.kernel_source_hash())") > "$OUT/kernel_src_sha16.txt"
+date -u +%Y-%m-%dT%H:%M:%SZ > "$OUT/collected_utc.txt"
 export TMPDIR=/tmp
 step() { echo "[$(date +%T)] $*"; }
 cd /tmp

@@ -9,8 +9,22 @@ FETCH_SIZE under-reports wide coalesced reads; WRITE_SIZE exact for streaming st
 import argparse
 import csv
 import json
+import os
+import time
 from statistics import mean
 
+
+
+def _stamp(d):
+    """Provenance of a summary: UTC collection time and the kernel-source hash of the tree it was collected
+    on (bench.kernel_source_hash), so bench.py can tell a bound from a stale profile."""
+    import sys as _sys
+    _sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    # the profiling run's own record (tools/profile_all.sh writes both on the box), else this tree's
+    d["collected_utc"] = os.environ.get("HMMBW_PROFILE_UTC") or time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime())
+    d["kernel_src_sha16"] = os.environ.get("HMMBW_PROFILE_SHA") or bench.kernel_source_hash()
+    return d
 
 def per_kernel(path, name_sub, counter):
     vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(path))
@@ -52,6 +66,7 @@ def main():
            "hbm_read_bytes_per_launch": rd, "hbm_write_bytes_per_launch": wr,
            "hbm_bytes_per_launch": rd + wr,
            "note": "L2-miss (fabric) bytes: Infinity-Cache hits are counted, as on every gfx950 PMC read"}
+    _stamp(out)
     with open(a.out, "w") as fh:
         json.dump(out, fh, indent=2)
     print(json.dumps(out))
