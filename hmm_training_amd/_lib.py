@@ -52,7 +52,6 @@ OPT_PEER_TIMEOUT_MS = 9
 OPT_LIVE_STATUS = 10
 OPT_WQ_TIMEOUT_MS = 11
 OPT_WIDE_WQ = 12
-OPT_WIDE_PAIR = 13
 INFO_WIDE_WQ_ACTIVE = 101
 INFO_WAVES = 102
 INFO_WORKGROUPS = 103
@@ -60,7 +59,6 @@ INFO_WAVES_PER_WORKGROUP = 104
 INFO_FULL_WORKGROUPS = 105
 INFO_EXTRA_WAVES = 106
 INFO_PEER_CHUNKS = 107
-INFO_WIDE_PAIRED = 108
 ALLREDUCE = {"rccl": 0, "peer": 1}
 
 

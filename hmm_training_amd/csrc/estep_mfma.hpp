@@ -95,51 +95,30 @@ __device__ __forceinline__ f64x4 mfma_f64(double a, double b, f64x4 c) {
 // loads even out in units of a sweep instead of a whole tile (cfg5 shard: 391 tiles on 256 CUs left 135
 // CUs two tiles and the others one).  A unit only waits for a unit taken before it, by a workgroup that
 // is running, so the waits always end.
-// LDS doubles of one tile's images and scratch (the host sizes the launch with the same formula)
-template <int NT, bool FWD_ONLY>
-__host__ __device__ constexpr int wide_tile_lds_doubles() {
-    return (FWD_ONLY ? 4 : 6) * 16 * NT * kXs + NT * kTileSeqs + 16;
-}
-
-// TP = 2 (paired tiles, E-step only): ONE workgroup of 2 NT waves runs two tiles, waves [0, NT) tile
-// 2b and waves [NT, 2 NT) tile 2b + 1, each with its own LDS images.  Both tiles' waves share the SIMDs
-// (two waves per SIMD, as two co-resident one-tile workgroups would), but their steps are held half a
-// step apart: every step is split by an extra barrier into its MFMA chain and its tail (the exchange
-// images, stores), and the second tile's waves start one barrier later, so on every SIMD one tile's
-// MFMA chain runs while the other tile's wave does its tail.  Two co-resident one-tile workgroups drift
-// into the same phase and measured 1.66x one tile's time; the host pairs tiles when they exceed the CUs
-// but not twice their count (the cfg5 shard: 391 tiles), one workgroup per CU.  The two tiles of a pair
-// are laid out with the same step count (the host raises the second's wave_T to the first's, its extra
-// steps masked), so both execute the same barriers.
-template <int NT, bool FWD_ONLY, bool DET = false, bool WQ = false, int TP = 1>
-__global__ void __launch_bounds__(NT * 64 * TP, 2) k_estep_mfma(EArgs a) {  // 2 waves per SIMD: <= 256 VGPRs
+template <int NT, bool FWD_ONLY, bool DET = false, bool WQ = false>
+__global__ void __launch_bounds__(NT * 64, 2) k_estep_mfma(EArgs a) {  // 2 waves per SIMD: <= 256 VGPRs
     static_assert(!(DET && FWD_ONLY), "deterministic mode is an E-step option");
     static_assert(!WQ || (!DET && !FWD_ONLY), "the work queue is an E-step option (atomic statistics)");
-    static_assert(TP == 1 || (TP == 2 && !WQ && !DET && !FWD_ONLY), "paired tiles: the atomic E-step");
     constexpr int NP = 16 * NT, KB = 4 * NT, IMG = NP * kXs, IMGX = 2 * IMG;
     extern __shared__ __attribute__((aligned(256))) double smem[];  // 256-B aligned whatever the static LDS (ds_read_b128 rows)
-    // this thread's tile of the workgroup (TP = 2: q = 0 / 1) and its index inside that tile's waves
-    const int q = TP == 2 ? (int)(threadIdx.x / (NT * 64)) : 0;
     // [2][2 NP][kXs]: z (forward) / v (backward) images, every row stored twice (rows r and r + NP), so that
     // wave m reads the other blocks in the order 16m + 16, ..., 16m + NP - 1 without wrapping (below)
-    double *X0 = smem + q * wide_tile_lds_doubles<NT, FWD_ONLY>();
-    double *Z0 = X0 + 2 * IMGX;                        // [2][NP][kXs] masked z (backward xi operand)
-    double *sRed = X0 + (FWD_ONLY ? 2 * IMGX : 2 * IMGX + 2 * IMG);  // [NT][16] partial sums + block LL scratch
-    // the workgroup-wide log-likelihood scratch (block_ll_partial over all TP x NT waves): tile 0's
-    double *sLL = smem + (FWD_ONLY ? 2 * IMGX : 2 * IMGX + 2 * IMG) + NT * kTileSeqs;
+    double *X0 = smem;
+    double *Z0 = smem + 2 * IMGX;                        // [2][NP][kXs] masked z (backward xi operand)
+    double *sRed = smem + (FWD_ONLY ? 2 * IMGX : 2 * IMGX + 2 * IMG);  // [NT][16] partial sums + block LL scratch
     if constexpr (!FWD_ONLY)  // clear the next iteration's statistics (single rank: triple buffer)
         for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < a.zero_len;
              i += (long long)gridDim.x * blockDim.x)
             a.zero[i] = 0.0;
     if (a.state != nullptr && a.state->done) return;    // converged: device-side no-op (:346)
     CHUNKSTAMP(0, 62);  // diagnostics build only (tools/wide_chunk_times.py): shader-clock stamps per chunk
-    const int tid = threadIdx.x - q * NT * 64, lane = tid & 63, m = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, m = tid >> 6;
     const int s = lane & 15, g = lane >> 4;
     const int N = a.N;
-    const long long ntile = WQ ? (long long)a.wq_units : (long long)gridDim.x * TP;
+    const long long ntile = WQ ? (long long)a.wq_units : (long long)gridDim.x;
     bool do_f = true;  // this workgroup runs the tile's forward sweep ...
     bool do_b = true;  // ... and its backward sweep
-    long long tile = (long long)blockIdx.x * TP + q;
+    long long tile = blockIdx.x;
     if constexpr (WQ) {
         __shared__ int s_unit;
         if (tid == 0) s_unit = (int)atomicAdd(a.wq, 1u);
@@ -281,7 +260,6 @@ __global__ void __launch_bounds__(NT * 64 * TP, 2) k_estep_mfma(EArgs a) {  // 2
 #pragma unroll
             for (int r = 0; r < 4; ++r) x[r] = __builtin_amdgcn_ldexp(acc[r], -sc) * b[r];
         }
-        if constexpr (TP == 2) __syncthreads();  // end of this step's chain half (the other tile's tail)
         if constexpr (MASK) {
             const bool act = t < T;  // past the sequence's end: z frozen at z_{T-1}
 #pragma unroll
@@ -338,8 +316,6 @@ __global__ void __launch_bounds__(NT * 64 * TP, 2) k_estep_mfma(EArgs a) {  // 2
         for (int c = cf > 1 ? cf : 1; c < nch; ++c) fchunk(c, MASK_, std::false_type{});
     };
     if (do_f) {
-        // paired tiles: the second tile's waves run one barrier behind the first's (half a step)
-        if constexpr (TP == 2) if (q == 1) __syncthreads();
         if (full) forward(std::false_type{});
         else forward(std::true_type{});
     } else if constexpr (WQ) {
@@ -525,7 +501,6 @@ __global__ void __launch_bounds__(NT * 64 * TP, 2) k_estep_mfma(EArgs a) {  // 2
                     else if (s == 0 && j < N && x != 0.0) unsafeAtomicAdd(&accb[j], x);
                 }
             }
-            if constexpr (TP == 2) __syncthreads();  // end of the chain half (the other tile's publish)
             next();  // publish(t - 1), when there is a step t - 1
         };
         uint4 pc;  // chunk c's symbol pack; chunk c - 1's is loaded at the top of chunk c
@@ -610,7 +585,7 @@ __global__ void __launch_bounds__(NT * 64 * TP, 2) k_estep_mfma(EArgs a) {  // 2
     if constexpr (WQ) {
         if (do_f) {  // the tile's log P pair, then the release of alpha_hat and s_t to its backward unit
             __syncthreads();
-            block_ll_partial(lp, ll_valid, sLL, a.llpart + 2 * tile);
+            block_ll_partial(lp, ll_valid, sRed + NT * kTileSeqs, a.llpart + 2 * tile);
             if constexpr (HMMBW_WQ_WT) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the stores have landed
             else __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
             __syncthreads();
@@ -634,9 +609,8 @@ __global__ void __launch_bounds__(NT * 64 * TP, 2) k_estep_mfma(EArgs a) {  // 2
         }
         return;
     }
-    if constexpr (TP == 2) if (q == 0) __syncthreads();  // both tiles' waves aligned again
     __syncthreads();
-    block_ll_partial(lp, ll_valid, sLL, a.llpart + 2 * (long long)blockIdx.x);
+    block_ll_partial(lp, ll_valid, sRed + NT * kTileSeqs, a.llpart + 2 * (long long)blockIdx.x);
     if constexpr (!DET && !FWD_ONLY) {
         // fused multi-rank launch (hmmbw_iterate / hmmbw_iterate_begin): the statistics went straight
         // into the all-reduce buffer; the last tile to finish folds the tiles' (max, sum exp) pairs

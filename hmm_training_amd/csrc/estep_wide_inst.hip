@@ -20,13 +20,6 @@ KernelFn wide_wq_kernel(int NP) {
     return nullptr;
 }
 
-KernelFn wide_pair_kernel(int NP) {
-    if (NP == 32) return k_estep_mfma<2, false, false, false, 2>;
-    if (NP == 48) return k_estep_mfma<3, false, false, false, 2>;
-    if (NP == 64) return k_estep_mfma<4, false, false, false, 2>;
-    return nullptr;
-}
-
 BnumFn bnum_gather_kernel(bool sorted) { return sorted ? k_bnum_gather<true> : k_bnum_gather<false>; }
 
 }  // namespace hmmbw

@@ -486,8 +486,6 @@ struct hmmbw_ctx {
     unsigned *d_wq = nullptr;  // wide work queue (EArgs::wq): 2 counters + a flag per tile, or nullptr
     long long wq_grid = 0;     // its grid (a workgroup per unit: 2 x tiles)
     int wq_mode = -1;          // HMMBW_OPT_WIDE_WQ: -1 auto (from 4 tiles per CU), 0 off, 1 on (more tiles than CUs)
-    int pair_mode = 0;         // HMMBW_OPT_WIDE_PAIR: -1 auto (tiles in (CUs, 2 CUs]), 0 off, 1 whenever tiles > 1
-    int wide_tp = 1;           // tiles per workgroup of the wide E-step of the loaded observations (1 or 2)
     long long wq_timeout_ms = 10000;  // HMMBW_OPT_WQ_TIMEOUT_MS: bound of a backward unit's wait
     uint4 *d_sp = nullptr;
     int *d_ebuf = nullptr;
@@ -791,13 +789,6 @@ int plan_estep(hmmbw_ctx *c, bool fwd_only, const IterState *state, double *copi
         p.fn = fwd_only ? kw.score : (c->det ? kw.det_estep : kw.estep);
         p.block = (unsigned)(nt * kWave);
         if (!p.fn) return fail(HMMBW_E_UNSUPPORTED, "no wide kernel for N");
-        if (!fwd_only && !c->det && !c->d_wq && c->wide_tp == 2) {  // paired tiles (estep_mfma.hpp, TP = 2)
-            p.fn = wide_pair_kernel(c->NP);
-            p.grid = (unsigned)(c->nblocks / 2);
-            p.block = (unsigned)(2 * nt * kWave);
-            p.lds *= 2;
-            if (!p.fn) return fail(HMMBW_E_UNSUPPORTED, "no wide paired-tile kernel for N");
-        }
         if (!fwd_only && !c->det && c->d_wq) {  // more tiles than CUs: the work-queue form (estep_mfma.hpp)
             p.fn = wide_wq_kernel(c->NP);
             p.grid = (unsigned)c->wq_grid;
@@ -1111,7 +1102,6 @@ int hmmbw_ctx_create(int device, int n_states, int n_symbols, hmmbw_ctx **out) {
     c->G = c->wide ? c->NP : (n_states <= 2 ? 2 : n_states <= 4 ? 4 : n_states <= 8 ? 8 : 16);
     c->U = c->wide ? 16 : kWave / c->G;
     if (const char *we = std::getenv("HMMBW_WIDE_WQ")) c->wq_mode = std::atoi(we) == 0 ? 0 : (std::atoi(we) == 1 ? 1 : -1);
-    if (const char *wp = std::getenv("HMMBW_WIDE_PAIR")) c->pair_mode = std::atoi(wp) == 0 ? 0 : (std::atoi(wp) == 1 ? 1 : -1);
     int rc = set_device(c);
     if (!rc) {
         int khz = 0;
@@ -1253,18 +1243,7 @@ int hmmbw_set_observations(hmmbw_ctx *c, const int64_t *offsets, const int32_t *
     std::iota(perm.begin(), perm.end(), 0);
     std::stable_sort(perm.begin(), perm.end(), [&](int64_t x, int64_t y) { return len[x] > len[y]; });
     const int U = c->U;
-    long long nwaves = (R + U - 1) / U;
-    // Wide path: paired tiles (k_estep_mfma<..., TP = 2>, estep_mfma.hpp) when the tiles exceed the CUs
-    // but not twice their count: one workgroup of two tiles per CU instead of two co-resident one-tile
-    // workgroups on some CUs and one on the others.  An odd tile count gets an all-padding tile, and the
-    // second tile of each pair is laid out with the first one's step count.
-    bool pair = false;
-    if (c->wide && !c->det && c->pair_mode != 0 && nwaves > 1) {
-        int ncu = 0;
-        (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device);
-        pair = c->pair_mode == 1 || (ncu > 0 && nwaves > ncu && nwaves <= 2LL * ncu);
-    }
-    if (pair && (nwaves & 1)) ++nwaves;
+    const long long nwaves = (R + U - 1) / U;
     std::vector<long long> wsym((size_t)nwaves), wck((size_t)nwaves), wsp((size_t)nwaves);
     std::vector<int> wT((size_t)nwaves), wfull((size_t)nwaves), slen((size_t)(nwaves * U), 0),
         sseq((size_t)(nwaves * U), -1);
@@ -1280,7 +1259,6 @@ int hmmbw_set_observations(hmmbw_ctx *c, const int64_t *offsets, const int32_t *
                 Tmin = std::min(Tmin, slen[(size_t)s]);
             }
         }
-        if (pair && (w & 1)) Tw = std::max(Tw, wT[(size_t)w - 1]);  // the pair's step count (sorted: the first's)
         const long long nch = (Tw + kChunk - 1) / kChunk;
         wT[(size_t)w] = Tw;
         wfull[(size_t)w] = (Tmin == Tw) ? 1 : 0;
@@ -1425,7 +1403,6 @@ int hmmbw_set_observations(hmmbw_ctx *c, const int64_t *offsets, const int32_t *
     c->nblocks = nblocks;
     c->nfull = nfull;
     c->xact = xact;
-    c->wide_tp = pair ? 2 : 1;
     if (const char *pe = std::getenv("HMMBW_PRIO")) c->prio = std::atoi(pe);
     c->has_obs = true;
     if (int rc2 = ensure_wq(c)) return rc2;
@@ -1502,12 +1479,6 @@ int hmmbw_set_option(hmmbw_ctx *c, int key, int64_t value) {
         c->wq_mode = (int)value;
         return ensure_wq(c);
     }
-    if (key == HMMBW_OPT_WIDE_PAIR) {
-        if (value < -1 || value > 1) return fail(HMMBW_E_INVALID, "HMMBW_OPT_WIDE_PAIR: -1 (auto), 0 (off) or 1 (on)");
-        if (c->has_obs) return fail(HMMBW_E_STATE, "set HMMBW_OPT_WIDE_PAIR before hmmbw_set_observations");
-        c->pair_mode = (int)value;
-        return HMMBW_OK;
-    }
     if (key == HMMBW_OPT_ABLATE) {  // diagnostics: results are wrong while set
         c->ablate = (int)value;
         return HMMBW_OK;
@@ -1530,10 +1501,8 @@ int hmmbw_get_option(const hmmbw_ctx *c, int key, int64_t *value) {
         case HMMBW_OPT_WIDE_WQ: *value = c->wq_mode; return HMMBW_OK;
         case HMMBW_INFO_WIDE_WQ_ACTIVE: *value = c->d_wq ? 1 : 0; return HMMBW_OK;
         case HMMBW_INFO_WAVES: *value = c->wide ? c->nblocks * (c->NP / 16) : c->nwaves; return HMMBW_OK;
-        case HMMBW_INFO_WORKGROUPS: *value = c->d_wq ? c->wq_grid : c->nblocks / (c->wide ? c->wide_tp : 1); return HMMBW_OK;
-        case HMMBW_INFO_WAVES_PER_WORKGROUP: *value = c->wide ? c->NP / 16 * (c->d_wq ? 1 : c->wide_tp) : kBlock / kWave; return HMMBW_OK;
-        case HMMBW_OPT_WIDE_PAIR: *value = c->pair_mode; return HMMBW_OK;
-        case HMMBW_INFO_WIDE_PAIRED: *value = (c->wide && !c->d_wq && c->wide_tp == 2) ? 1 : 0; return HMMBW_OK;
+        case HMMBW_INFO_WORKGROUPS: *value = c->d_wq ? c->wq_grid : c->nblocks; return HMMBW_OK;
+        case HMMBW_INFO_WAVES_PER_WORKGROUP: *value = c->wide ? c->NP / 16 : kBlock / kWave; return HMMBW_OK;
         case HMMBW_INFO_FULL_WORKGROUPS: *value = c->wide ? c->nblocks : std::min(c->nfull, c->nblocks); return HMMBW_OK;
         case HMMBW_INFO_EXTRA_WAVES: *value = c->wide ? 0 : c->xact; return HMMBW_OK;
         case HMMBW_INFO_PEER_CHUNKS: *value = c->d_peer ? c->peer_nch : 0; return HMMBW_OK;

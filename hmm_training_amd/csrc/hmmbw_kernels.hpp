@@ -28,7 +28,6 @@ Kernels small_kernels_n(bool lr, bool ldstab);
 // Wide kernels (16 < N <= 64) for the padded state count NP (32, 48 or 64).
 Kernels wide_kernels(int NP);
 KernelFn wide_wq_kernel(int NP);  // the work-queue E-step (persistent grid, forward / backward units)
-KernelFn wide_pair_kernel(int NP);  // the paired-tile E-step (two tiles per workgroup, half a step apart)
 
 // The wide path's B-numerator gather (estep_mfma.hpp).
 using BnumFn = void (*)(const double *, const unsigned *, const long long *, int, int, int, double *, const IterState *);

@@ -284,19 +284,12 @@ class BaumWelchEngine:
         return {"waves": self.get_option(INFO_WAVES), "workgroups": self.get_option(INFO_WORKGROUPS),
                 "waves_per_workgroup": self.get_option(INFO_WAVES_PER_WORKGROUP),
                 "full_workgroups": self.get_option(INFO_FULL_WORKGROUPS),
-                "extra_waves": self.get_option(INFO_EXTRA_WAVES), "work_queue": self.work_queue_active,
-                "paired_tiles": self.paired_tiles_active}
+                "extra_waves": self.get_option(INFO_EXTRA_WAVES), "work_queue": self.work_queue_active}
 
     def peer_chunks(self) -> int:
         """Chunks of the peer all-reduce payload (one flag per (rank, chunk) per iteration), 0 without a region."""
         from ._lib import INFO_PEER_CHUNKS
         return self.get_option(INFO_PEER_CHUNKS)
-
-    @property
-    def paired_tiles_active(self) -> bool:
-        """True if the wide E-step of the loaded observations runs as paired tiles (HMMBW_INFO_WIDE_PAIRED)."""
-        from ._lib import INFO_WIDE_PAIRED
-        return self.get_option(INFO_WIDE_PAIRED) == 1
 
     @property
     def work_queue_active(self) -> bool:

@@ -35,8 +35,7 @@ extern "C" {
 #define HMMBW_ABI_VERSION 5 /* 2: hmmbw_iterate_begin/_end, status snapshots, comm info/payload;
                               3: peer all-reduce (hmmbw_peer_*), HMMBW_E_TIMEOUT, cache trim, split timing;
                               4: live status mirror (HMMBW_OPT_LIVE_STATUS, hmmbw_status_live_wait);
-                              5: hmmbw_get_option, HMMBW_OPT_WQ_TIMEOUT_MS, HMMBW_OPT_WIDE_WQ,
-                                 HMMBW_OPT_WIDE_PAIR */
+                              5: hmmbw_get_option, HMMBW_OPT_WQ_TIMEOUT_MS, HMMBW_OPT_WIDE_WQ */
 
 #define HMMBW_OK 0
 #define HMMBW_E_INVALID (-1)        /* bad argument (shape, range, null pointer)             */
@@ -277,12 +276,6 @@ int hmmbw_score(hmmbw_ctx *ctx, double *out);
  * tiles exceed 4 per CU, 1 whenever they exceed the CU count, 0 never.  The environment variable
  * HMMBW_WIDE_WQ=0/1 sets a new context's default.  Takes effect at once. */
 #define HMMBW_OPT_WIDE_WQ 12
-/* Paired tiles of the wide E-step: one workgroup runs two 16-sequence tiles, their steps held half a step
- * apart so that one tile's MFMA chain runs while the other exchanges its images: -1 (default) when the
- * tiles exceed the CU count but not twice it (one such workgroup per CU), 1 whenever there are two tiles,
- * 0 never.  The environment variable HMMBW_WIDE_PAIR=0/1 sets a new context's default.  Set it before
- * hmmbw_set_observations (HMMBW_E_STATE after). */
-#define HMMBW_OPT_WIDE_PAIR 13
 int hmmbw_set_option(hmmbw_ctx *ctx, int key, int64_t value);
 /* The current value of an option above, or a read-only fact about the loaded observations' E-step launch:
  * HMMBW_INFO_WIDE_WQ_ACTIVE    1 if it runs on the wide work queue;
@@ -303,7 +296,6 @@ int hmmbw_set_option(hmmbw_ctx *ctx, int key, int64_t value);
 #define HMMBW_INFO_FULL_WORKGROUPS 105
 #define HMMBW_INFO_EXTRA_WAVES 106
 #define HMMBW_INFO_PEER_CHUNKS 107
-#define HMMBW_INFO_WIDE_PAIRED 108 /* 1 if the wide E-step runs as paired tiles (HMMBW_OPT_WIDE_PAIR) */
 int hmmbw_get_option(const hmmbw_ctx *ctx, int key, int64_t *value);
 
 /* E-step kernel timing with HIP events on the context stream (for bench/roofline).  Returns the

@@ -100,8 +100,7 @@ def statistics_pass(eng, N, K, R):
     return g, ll, eng.params(normalise=False)
 
 
-def run_vs_oracle(oracle, R, T, N, K, topology, iters, seed, symbols="U", deterministic=False, work_queue=None,
-                  paired=None):
+def run_vs_oracle(oracle, R, T, N, K, topology, iters, seed, symbols="U", deterministic=False, work_queue=None):
     from hmm_training_amd.engine import BaumWelchEngine, StatsLayout
     sym = _symbols(R, T, N, K, symbols, seed)
     off = np.arange(R + 1, dtype=np.int64) * T
@@ -115,8 +114,6 @@ def run_vs_oracle(oracle, R, T, N, K, topology, iters, seed, symbols="U", determ
         assert eng.topology == topology
         if work_queue is not None:  # which wide E-step form the library chose on its own (no option set)
             assert eng.work_queue_active == work_queue
-        if paired is not None:
-            assert eng.paired_tiles_active == paired
         # -------- production iterations, enqueued together (merged M-steps) --------
         eng.reset(0.0, iters)
         eng.enqueue_iterations(iters)
@@ -172,10 +169,8 @@ def test_cfg5_full_shape_slice_vs_oracle(oracle_mt):
 
 
 def test_cfg5_shard_full_size_vs_oracle(oracle_mt):
-    """BASELINE cfg5's per-GPU shard: 6,250 x T=400, N=64, K=1024, dense, 2 EM iterations vs the oracle.
-    391 tiles: paired (two tiles per workgroup, estep_mfma.hpp TP = 2; 196 workgroups, the last with an
-    all-padding partner)."""
-    run_vs_oracle(oracle_mt, 6_250, 400, 64, 1024, "dense", 2, seed=5, paired=True)
+    """BASELINE cfg5's per-GPU shard: 6,250 x T=400, N=64, K=1024, dense, 2 EM iterations vs the oracle."""
+    run_vs_oracle(oracle_mt, 6_250, 400, 64, 1024, "dense", 2, seed=5)
 
 
 def test_wide_work_queue_one_context_full_size_vs_oracle(oracle_mt):

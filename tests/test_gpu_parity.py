@@ -191,38 +191,6 @@ def test_wide_work_queue_vs_oracle(N, equal, wq, oracle, monkeypatch):
     assert_params(p2, ref.pi, "pi")
 
 
-@pytest.mark.parametrize("N,R,tmax,equal", [(24, 37, 60, False), (40, 99, 50, False), (64, 53, 40, True),
-                                             (64, 83, 48, False)])
-def test_wide_paired_tiles_vs_oracle(N, R, tmax, equal, oracle, monkeypatch):
-    """The wide E-step with two 16-sequence tiles per workgroup, held half a step apart (estep_mfma.hpp,
-    TP = 2; HMMBW_WIDE_PAIR=1 forces it at any tile count): odd tile counts (an all-padding partner tile),
-    ragged lengths whose pairs differ in length (the second tile runs the first one's steps, masked), and
-    equal lengths; 3 EM iterations against the oracle (hmm_training.py:351-514)."""
-    from hmm_training_amd.engine import BaumWelchEngine, to_csr
-    monkeypatch.setenv("HMMBW_WIDE_PAIR", "1")
-    K = 64
-    rng = np.random.default_rng(7 * N + R)
-    obs, pi, A, B = random_problem(rng, N, K, R=R, tmax=tmax, topology="dense")
-    if equal:
-        obs = [rng.integers(0, K, size=tmax) for _ in range(R)]
-    off, sym = to_csr(obs)
-    ref = oracle.hmm_training(off, sym.astype(np.int64), N, K, 1e-9, 3, pi, A, B)
-    with BaumWelchEngine(N, K, topology="dense") as eng:
-        eng.set_observations(obs)
-        eng.set_params(pi, A, B)
-        assert eng.paired_tiles_active
-        lm = eng.launch_map()
-        assert lm["workgroups"] == (-(-R // 16) + 1) // 2 and lm["waves_per_workgroup"] == 2 * (-(-N // 16))
-        trace = []
-        eng.train(1e-9, 3, lambda k, L, df: trace.append(L))
-        assert_ll(trace, ref.trace_L)
-        assert_ll(eng.loglik(), ref.logP)
-        p2, A2, B2 = eng.params(normalise=True)
-    assert_params(A2, ref.A, "A")
-    assert_params(B2, ref.B, "B")
-    assert_params(p2, ref.pi, "pi")
-
-
 def test_wide_work_queue_timeout_is_an_error(oracle):
     """The work queue's bounded wait (estep_mfma.hpp): a backward sweep whose forward has not finished
     within HMMBW_OPT_WQ_TIMEOUT_MS stops EM with HMMBW_E_TIMEOUT, reported by the status calls, instead of

@@ -8,7 +8,7 @@ mkdir -p $O
 export PYTHONUNBUFFERED=1
 step() { echo "[$(date +%T)] $*"; }
 step pytest
-timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread \
+HMMBW_WIDE_PAIR=-1 timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread \
   tests/test_gpu_parity.py tests/test_gpu_fullsize.py tests/test_gpu_multirank.py \
   -k "wide or cfg5_shard or cfg5_full_shape or work_queue or multirank" > $O/pytest.log 2>&1
 rc=$?; tail -3 $O/pytest.log; [ $rc -ne 0 ] && exit $rc
