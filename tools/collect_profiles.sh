@@ -15,6 +15,7 @@ declare -A KEY=([lr_cfg3]=R10000_T200_N8_K256_left_to_right [lrH_cfg3]=R10000_T2
 declare -A KER=([lr_cfg3]=k_estep_small [lrH_cfg3]=k_estep_small [dense_cfg3]=k_estep_small
                 [cfg5]="k_estep_mfma,k_bnum_gather" [cfg4shard]=k_estep_small)
 for W in lr_cfg3 lrH_cfg3 dense_cfg3 cfg5 cfg4shard; do
+  [ -d "$SRC/trace_$W" ] || { echo "skip $W (not in this run)"; continue; }
   cp "$SRC/trace_$W/run_kernel_stats.csv" "profiles/$DEST/kernel_stats_$W.csv"
   for C in FETCH_SIZE WRITE_SIZE SQ SQ2; do
     cp "$SRC/pmc_${C}_$W/run_counter_collection.csv" "profiles/$DEST/pmc_${C}_$W.csv"
@@ -27,8 +28,9 @@ for W in lr_cfg3 lrH_cfg3 dense_cfg3 cfg5 cfg4shard; do
     --kernel-stats "profiles/$DEST/kernel_stats_$W.csv" > "profiles/$DEST/sq_$W.json"
 done
 for W in cfg2 vq; do
-  cp "$SRC/trace_$W/run_kernel_stats.csv" "profiles/$DEST/kernel_stats_$W.csv"
+  [ -d "$SRC/trace_$W" ] && cp "$SRC/trace_$W/run_kernel_stats.csv" "profiles/$DEST/kernel_stats_$W.csv"
 done
+[ -f "$SRC/bench_full.log" ] || exit 0  # part a: no bench lines
 grep -h '"metric"' "$SRC/bench_full.log" > "profiles/$DEST/bench_lr_cfg3.json"
 grep -h '"metric"' "$SRC/bench_dense.log" > "profiles/$DEST/bench_dense_cfg3.json"
 grep -h '"metric"' "$SRC/bench_H.log" > "profiles/$DEST/bench_lrH_cfg3.json"
