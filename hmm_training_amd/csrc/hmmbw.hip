@@ -701,11 +701,33 @@ int flush_mstep(hmmbw_ctx *c) {
     return HMMBW_OK;
 }
 
+// The largest dynamic LDS each kernel has been allowed so far on each device: hipFuncSetAttribute once
+// per kernel and size, not on every launch (the LR cfg3 launch asks for 66,880 B every EM iteration).
+struct LdsGrants {
+    std::mutex mu;
+    std::map<std::pair<int, const void *>, size_t> have;
+};
+LdsGrants &lds_grants() {
+    static LdsGrants g;
+    return g;
+}
+
+int allow_lds(const void *f, size_t lds) {
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev));
+    LdsGrants &g = lds_grants();
+    std::lock_guard<std::mutex> lk(g.mu);
+    size_t &have = g.have[std::make_pair(dev, f)];
+    if (have >= lds) return HMMBW_OK;
+    HIP_TRY(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    have = lds;
+    return HMMBW_OK;
+}
+
 template <class F>
 int launch_lds(F f, unsigned grid, size_t lds, hipStream_t stream, const EArgs &a, unsigned block = kBlock) {
     if (lds > 64 * 1024)
-        HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(f), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    (int)lds));
+        if (int rc = allow_lds(reinterpret_cast<const void *>(f), lds)) return rc;
     hipLaunchKernelGGL(f, dim3(grid), dim3(block), lds, stream, a);
     HIP_TRY(hipGetLastError());
     return HMMBW_OK;

@@ -277,7 +277,8 @@ __device__ __forceinline__ void fmac_bcast1(double &acc, double z, double a) {
 // inside the asm, so the first fused product after z is written goes behind this.
 __device__ __forceinline__ void dpp_guard(double z) { asm volatile("s_nop 1" ::"v"(z)); }
 
-// acc0 += sum over even i of a[i] z(lane i), acc1 the odd i (two chains), per G-lane group
+// acc0 += sum over even i of a[i] z(lane i), acc1 the odd i (two chains), per G-lane group.  (Four
+// chains, i mod 4, measured slower at dense cfg3: 76-77 against 71-73 us, profiles/r5/ab_dense_dot4.txt.)
 template <int G, int N>
 __device__ __forceinline__ void bcast_dot(double &acc0, double &acc1, double z, const double (&a)[N]) {
     dpp_guard(z);
@@ -345,7 +346,7 @@ __device__ __forceinline__ char *lds_ptr(unsigned a) {
 
 // Per-block (max, sum exp(x - max)) of the sequences' log P (each sequence contributes from
 // exactly one lane with valid = true).  All threads of the block call it.
-__device__ void block_ll_partial(double lp, bool valid, double *sh, double *out) {
+__device__ __forceinline__ void block_ll_partial(double lp, bool valid, double *sh, double *out) {
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, nw = blockDim.x >> 6;
     double m = valid ? lp : -INFINITY;
     for (int k = 32; k >= 1; k >>= 1) m = fmax(m, __shfl_xor(m, k));
@@ -425,9 +426,9 @@ __device__ __forceinline__ void tab_put(double *sP, double *sH, int i, double px
 }
 
 template <int N, int G, int GP, bool PT, int BLK = kBlock>
-__device__ bool merged_mstep(const EArgs &a, double *sP, double *sH, double *sPA, long long bid);
-__device__ int rank_ll_count(const EArgs &a);
-__device__ void rank_ll_fold(const EArgs &a, long long nblk);
+__device__ __forceinline__ bool merged_mstep(const EArgs &a, double *sP, double *sH, double *sPA, long long bid);
+__device__ __forceinline__ int rank_ll_count(const EArgs &a);
+__device__ __forceinline__ void rank_ll_fold(const EArgs &a, long long nblk);
 
 // Body of the small-N E-step / scorer for workgroup `bid` of the `nblk` workgroups that cover one
 // model's sequences: the whole grid of k_estep_small, or one model's slice of a grouped launch
@@ -1526,12 +1527,12 @@ __device__ __forceinline__ double wave_max(double x) {
 // in its own launch).  No __threadfence: a device-scope release writes back the XCD's L2 (this launch's
 // checkpoints), which cost ~20 us per launch; the pairs are memory-side atomics, so thread 0 only has
 // to see its own pair land (vmcnt(0)) before it counts, and the folding wave reads them with atomics.
-__device__ int rank_ll_count(const EArgs &a) {
+__device__ __forceinline__ int rank_ll_count(const EArgs &a) {
     __builtin_amdgcn_s_waitcnt(0x0F70);  // s_waitcnt vmcnt(0): block_ll_partial's atomicExch has landed
     return atomicAdd(a.done_ctr, 1);
 }
 
-__device__ void rank_ll_fold(const EArgs &a, long long nblk) {  // one wave
+__device__ __forceinline__ void rank_ll_fold(const EArgs &a, long long nblk) {  // one wave
     const int lane = threadIdx.x & 63;
     double tm = -INFINITY, ts = 0.0;
     for (long long r0 = 0; r0 < nblk; r0 += 4 * 64) {
@@ -1563,7 +1564,7 @@ __device__ void rank_ll_fold(const EArgs &a, long long nblk) {  // one wave
 }
 
 template <int N, int G, int GP, bool PT, int BLK>
-__device__ bool merged_mstep(const EArgs &a, double *sP, double *sH, double *sPA, long long bid) {
+__device__ __forceinline__ bool merged_mstep(const EArgs &a, double *sP, double *sH, double *sPA, long long bid) {
     constexpr int NSM = N + N * N + 2 * N;  // pi_num, xi, gamma_den_excl, gamma_den_all
     constexpr int NW = BLK / 64;
     constexpr int SB = kMergedMaxStats / BLK;
