@@ -75,6 +75,11 @@ def parse(argv=None):
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=200)
     p.add_argument("--warmup", type=int, default=10)
+    p.add_argument("--prewarm-ms", type=float, default=200.0,
+                   help="untimed EM iterations for at least this long before the warm-up steps: the GPU clocks "
+                        "ramp up over ~35 ms of load after the set-up (profiles/r5/warmup_ramp.txt)")
+    p.add_argument("--trace-region", action="store_true",
+                   help="print host timestamps of the timed region (diagnostics, stderr)")
     p.add_argument("--workload", default="auto", choices=["auto", *WORKLOADS],
                    help="auto: cfg3 on one GPU, cfg4 shards (12,500 per GPU) on several")
     p.add_argument("--R", type=int, default=None, help="sequences per GPU (overrides the workload)")
@@ -512,6 +517,24 @@ def main(argv=None):
         eng.enqueue_iterations(n, stats)
         n_iter[0] += n
 
+    def prewarm(ms):
+        """Untimed iterations for about `ms` of GPU work: one batch of 20 measures the iteration time, then
+        every rank enqueues the same count (the largest over ranks: each iteration is a collective)."""
+        if ms <= 0:
+            return
+        t_start = time.perf_counter()
+        enqueue(20)
+        torch.cuda.synchronize()
+        per = max((time.perf_counter() - t_start) / 20, 1e-6)
+        n = min(int(ms / 1000.0 / per), 200_000)
+        if world > 1:
+            t = torch.tensor([n], dtype=torch.int64, device=f"cuda:{device}" if args.dist_backend == "nccl" else "cpu")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            n = int(t.item())
+        if n > 20:
+            enqueue(n - 20)
+        torch.cuda.synchronize()
+
     def leg(steps, warmup):
         """Warm-up, then EXACTLY `steps` EM iterations between barrier + synchronize brackets (max over
         ranks), then the per-launch timing batch (HIP events) outside the timed region."""
@@ -522,17 +545,26 @@ def main(argv=None):
         # The engine launches on torch's current stream (BaumWelchEngine binds it), so one event pair on
         # that stream around the whole timed region gives the GPU time per step without perturbing it.
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ev0.record()  # the HIP events are created at their first record (~30 us of host time): not in the region
+        ev1.record()
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         ev0.record()
+        t_ev0 = time.perf_counter()
         enqueue(steps)  # one hmmbw_iterate(steps): the host enqueues the K launches back to back
+        t_enq = time.perf_counter()
         ev1.record()
         torch.cuda.synchronize()
+        t_sync = time.perf_counter()
         if world > 1:
             dist.barrier()
         elapsed = time.perf_counter() - t0
+        if args.trace_region:
+            print(f"[trace rank {rank}] ev0.record {1e6 * (t_ev0 - t0):.1f} us, enqueue({steps}) "
+                  f"{1e6 * (t_enq - t_ev0):.1f} us, ev1.record + sync {1e6 * (t_sync - t_enq):.1f} us, "
+                  f"region {1e6 * elapsed:.1f} us, GPU {1e3 * ev0.elapsed_time(ev1):.1f} us", file=sys.stderr, flush=True)
         r = {"gpu_ms_step": ev0.elapsed_time(ev1) / steps, "kern_ms": 0.0, "kern_n": 0, "est_ms": 0.0, "est_n": 0,
              "ar_ms": 0.0, "ar_n": 0}
         # a device-side failure (a peer all-reduce timeout) is recorded, not raised, until every rank has
@@ -574,6 +606,7 @@ def main(argv=None):
         return r
 
     legs, failed = {}, {}
+    prewarm(args.prewarm_ms)
     first = leg(args.steps, args.warmup)
     if first["error"]:
         raise RuntimeError(first["error"])
