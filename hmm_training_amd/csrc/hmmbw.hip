@@ -473,6 +473,7 @@ struct hmmbw_ctx {
     long long nfull = 0;          // small kernels: workgroups with 4 active waves (then xact-wave ones)
     int xact = 4;
     int prio = 2;                 // wave priority of the small kernels (EArgs::prio); HMMBW_PRIO overrides it
+    int split_extra = 1;          // EArgs::split_extra (HMMBW_SPLIT_EXTRA=0 turns it off)
     uint16_t *d_sym = nullptr;
     long long *d_wsym = nullptr, *d_wckoff = nullptr, *d_wspoff = nullptr;
     int *d_wT = nullptr, *d_wfull = nullptr, *d_slen = nullptr, *d_sseq = nullptr;
@@ -644,6 +645,7 @@ EArgs make_eargs(hmmbw_ctx *c) {
     a.nfull = c->nfull;
     a.xact = c->xact;
     a.prio = c->prio;
+    a.split_extra = c->split_extra;
     return a;
 }
 
@@ -1426,6 +1428,7 @@ int hmmbw_set_observations(hmmbw_ctx *c, const int64_t *offsets, const int32_t *
     c->nfull = nfull;
     c->xact = xact;
     if (const char *pe = std::getenv("HMMBW_PRIO")) c->prio = std::atoi(pe);
+    if (const char *se = std::getenv("HMMBW_SPLIT_EXTRA")) c->split_extra = std::atoi(se) != 0;
     c->has_obs = true;
     if (int rc2 = ensure_wq(c)) return rc2;
     return ensure_zf(c);

@@ -177,6 +177,9 @@ struct EArgs {
     // second wave on their SIMDs (cfg3 34.5-34.7 us per iteration against 36.0-36.8 at 0, two interleaved
     // rounds; no effect without extra waves, e.g. 12,500 sequences); 1 = for the full workgroups' waves
     int prio;
+    // split extra waves (small kernels, LDS tables): the idle waves of the spread map's extra workgroups run
+    // the lower half of their partner's backward sweep (estep_small_body, "split"); 0 off
+    int split_extra;
     // wide work queue (k_estep_mfma<..., WQ>): [0] next unit, [1] workgroups done; per-tile forward flags
     unsigned *wq;
     unsigned *wq_flag;
@@ -454,6 +457,10 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
     constexpr int GP = LDSTAB ? G + kTabPad : G;  // row stride of the emission / histogram tables
     // left-to-right with LDS tables: per (symbol, state) products {a_jj b_j(o), a_{j-1,j} b_j(o)}
     constexpr bool PT = LR && LDSTAB;
+    // split extra waves possible in this instantiation: dense E-step with LDS tables and atomic statistics
+    // (dense cfg3 69.4 -> 64.3 us; left-to-right 34.0 -> 35.6 us, and its code alone costs registers:
+    // profiles/r5/split_extra_ab.txt)
+    constexpr bool SPLITOK = !LR && LDSTAB && !FWD_ONLY && !DET;
     extern __shared__ __attribute__((aligned(256))) double smem[];  // 256-B aligned whatever the static LDS (ds_read_b128 rows)
     __shared__ double sPA[G + N * N];  // pi (zero-padded to G) and A of this iteration
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -471,8 +478,13 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
     if constexpr (LDSTAB && !FWD_ONLY) merged = a.merged != 0;
     const int wpb = blockDim.x >> 6;
     const bool xblk = bid >= a.nfull;
-    const long long wave = xblk ? a.nfull * wpb + (bid - a.nfull) * a.xact + wv : bid * wpb + wv;
-    const bool wactive = !xblk || wv < a.xact;
+    // split extra waves: in an extra workgroup with 2 xact <= 4 waves, wave wv in [xact, 2 xact) is the B
+    // partner of wave wv - xact (same sequence group): it runs the lower half of the group's backward
+    const bool split_wg = SPLITOK && xblk && a.split_extra != 0 && 2 * a.xact <= wpb;
+    const bool brole = split_wg && wv >= a.xact && wv < 2 * a.xact;
+    const int wvg = brole ? wv - a.xact : wv;
+    const long long wave = xblk ? a.nfull * wpb + (bid - a.nfull) * a.xact + wvg : bid * wpb + wv;
+    const bool wactive = !xblk || wv < a.xact || brole;
     if (merged) {
         // the previous iteration's M-step, computed redundantly by every workgroup straight into
         // its LDS tables (no separate M-step kernel, no parameter round trip through HBM)
@@ -622,6 +634,71 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
         // Lagged mode: only steps t = 0 mod kScale rescale; s_t = M_{t-kScale}, the group exponent
         // measured right after step t-kScale, so C_t = log2|alpha_{t-kScale}| and the stored z stay
         // within a few steps' growth of 1.
+        // split: the group's backward is cut at chunk hc (the B partner takes chunks [0, hc)); full waves of
+        // at least two chunks only
+        const bool spl = split_wg && full && nch >= 2;
+        const int hc = spl ? nch / 2 : -1;
+        int Ch = 0;  // C after step 8 hc (the forward records it)
+        // B partner: beta over t = Tw - 1 .. h with its own power-of-two scaling (beta_t = bt 2^Eb), no
+        // statistics (the recursion of :163-199 needs no alpha): the lower half's starting vector
+        auto presweep = [&](int h, int &Eb) -> double {
+            double bt = jv ? 1.0 : 0.0;
+            Eb = 0;
+            const int ctop = (Tw - 1) / kChunk, cbot = h / kChunk;
+            auto pchunk = [&](int c, const uint4 &p) {
+                Em ev[kChunk];
+#pragma unroll
+                for (int k = 0; k < kChunk; ++k) ev[k] = ld_em(p, k);
+#pragma unroll
+                for (int k = kChunk - 1; k >= 0; --k) {
+                    const int t1 = c * kChunk + k;  // beta_{t1 - 1} from beta_{t1} and b(o_{t1})
+                    double bn = bt;
+                    if constexpr (PT) {
+                        bn = fma(ev[k].x, bt, dpp<0x101>(ev[k].y * bt));  // row_shl:1: state j + 1
+                    } else if constexpr (!LR) {
+                        const double vd = ev[k] * bt;
+                        double b0 = 0.0, b1 = 0.0;
+                        if constexpr (G >= 4) {
+                            bcast_dot<G, N>(b0, b1, vd, arow);
+                        } else {
+                            sfor<0, N>([&](auto I) {
+                                const double vk = gbcast<G, I.value>(vd, lane);
+                                if constexpr ((I.value & 1) == 0) b0 = fma(arow[I.value], vk, b0);
+                                else b1 = fma(arow[I.value], vk, b1);
+                            });
+                        }
+                        bn = b0 + b1;
+                    }
+                    bt = (t1 >= h + 1 && t1 <= Tw - 1) ? bn : bt;
+                }
+                const int M = group_bexp(bt);
+                const int e = M == 0 ? 0 : M - 1023;
+                bt = pow2_scale(bt, e);
+                Eb += e;
+            };
+            // 4-deep pack ring, unrolled by 4 (no dynamic register indexing)
+            uint4 Q0 = loadpack(ctop), Q1 = loadpack(max(ctop - 1, cbot)), Q2 = loadpack(max(ctop - 2, cbot)),
+                  Q3 = loadpack(max(ctop - 3, cbot));
+            int c = ctop;
+            for (; c - 3 >= cbot; c -= 4) {
+                pchunk(c, Q0);
+                Q0 = loadpack(max(c - 4, cbot));
+                pchunk(c - 1, Q1);
+                Q1 = loadpack(max(c - 5, cbot));
+                pchunk(c - 2, Q2);
+                Q2 = loadpack(max(c - 6, cbot));
+                pchunk(c - 3, Q3);
+                Q3 = loadpack(max(c - 7, cbot));
+            }
+            if (c >= cbot) {
+                pchunk(c, Q0);
+                if (c - 1 >= cbot) {
+                    pchunk(c - 1, Q1);
+                    if (c - 2 >= cbot) pchunk(c - 2, Q2);
+                }
+            }
+            return bt;
+        };
         double z = 0.0;
         int C = 0;
         auto forward = [&](auto SAFE_, auto RAG_) -> bool {
@@ -681,6 +758,7 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
                         z = zn;
                         C += st;
                     }
+                    if (SPLITOK && k == 0) Ch = (c == hc) ? C : Ch;  // split: C_h, h = 8 hc
                     sp[k] = st;
                     if constexpr (!FWD_ONLY) {
                         if (ZF) {  // every z_t
@@ -747,33 +825,72 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
             return (!SAFE) && (minM < 1023 - 900 || maxM > 1023 + 900);
         };
         bool safe = a.force_safe != 0;
-        if (!safe) {
-            const bool bad = full ? forward(std::false_type{}, std::false_type{})
-                                  : forward(std::false_type{}, std::true_type{});
-            safe = __any(bad && T > 0) != 0;  // wave-uniform: redo the wave with per-step normalisation
-        }
-        if (safe) {
-            if (full) forward(std::true_type{}, std::false_type{});
-            else forward(std::true_type{}, std::true_type{});
+        if (!brole) {  // the B partner of a split group runs no forward
+            if (!safe) {
+                const bool bad = full ? forward(std::false_type{}, std::false_type{})
+                                      : forward(std::false_type{}, std::true_type{});
+                safe = __any(bad && T > 0) != 0;  // wave-uniform: redo the wave with per-step normalisation
+            }
+            if (safe) {
+                if (full) forward(std::true_type{}, std::false_type{});
+                else forward(std::true_type{}, std::true_type{});
+            }
         }
 
         PHASE(2);
         // log P(O|lambda) = log(sum_j z_{T-1}(j)) + ln2 * C   (:375-377)
-        const double phat = gsum<G>(z);
-        const bool alive = (T > 0) && (phat > 0.0);
-        const double lp = alive ? (log(phat) + (double)C * 0.69314718055994530942) : -INFINITY;
-        if (T > 0 && j == 0 && seq >= 0) a.logp[seq] = lp;
-        logp_lane = lp;
-        ll_valid = (T > 0) && (j == 0);
+        double phat = 0.0;
+        bool alive = false;
+        if (!brole) {
+            phat = gsum<G>(z);
+            alive = (T > 0) && (phat > 0.0);
+            const double lp = alive ? (log(phat) + (double)C * 0.69314718055994530942) : -INFINITY;
+            if (T > 0 && j == 0 && seq >= 0) a.logp[seq] = lp;
+            logp_lane = lp;
+            ll_valid = (T > 0) && (j == 0);
+        }
 
-        if constexpr (!FWD_ONLY) if (!(a.ablate & 2)) {
+        // ---- split extra waves: B's starting vector for the lower half, beta_hat at h = 8 hc ----
+        // beta_hat_t = beta_t 2^{C_t} / P (the forward's scaling), P = phat 2^{C_{T-1}}, so
+        // beta_hat_h = bt 2^{Eb - (C_{T-1} - C_h)} / phat.  One workgroup barrier (every wave of the
+        // workgroup passes it once) orders the forward's checkpoints, exponents and (1/phat, C_{T-1} - C_h,
+        // safe) before B reads them.
+        double beta_h = 0.0;
+        if constexpr (SPLITOK) if (split_wg) {
+            __shared__ double sXinv[kBlock / kWave / 2][kWave];
+            __shared__ int sXd[kBlock / kWave / 2][kWave];
+            __shared__ int sXsafe[kBlock / kWave / 2];
+            int Eb = 0;
+            double bt = 0.0;
+            if (brole && spl) bt = presweep(hc * kChunk, Eb);
+            if (!brole && spl) {
+                sXinv[wvg][lane] = alive ? 1.0 / phat : 0.0;
+                sXd[wvg][lane] = C - Ch;
+                if (lane == 0) sXsafe[wvg] = safe ? 1 : 0;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __syncthreads();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            if (brole && spl) {
+                safe = sXsafe[wvg] != 0;
+                beta_h = __builtin_amdgcn_ldexp(bt, Eb - sXd[wvg][lane]) * sXinv[wvg][lane];
+            }
+        }
+
+        if constexpr (!FWD_ONLY) if (!(a.ablate & 2)) if (!brole || spl) {
             // ------------- backward sweep fused with gamma / xi / M-step numerators -------------
             const double inv_p = alive ? 1.0 / phat : 0.0;  // beta_hat_{T-1}: folds 1/P (:392,:407)
-            auto backward = [&](auto SAFE_, auto RAG_) {
+            // chunks ctop down to clo, entering with beta_hat_{8 ctop + 8} = beta0 (the whole sweep: the top
+            // chunk (Tw - 1) / 8 down to 0 from 1/phat; split: A the top down to hc, B hc - 1 down to 0)
+            auto backward = [&](auto SAFE_, auto RAG_, auto SPLIT_, const int ctop_, const int clo_, const double beta0) {
                 constexpr bool SAFE = decltype(SAFE_)::value;
                 constexpr bool RAG = decltype(RAG_)::value;
-                double beta = inv_p;
-                const int cl = (Tw - 1) / kChunk;
+                // SPLIT: a part of the sweep (split groups only); otherwise the whole sweep, fixed at compile
+                // time, so the unsplit waves run the same code as without the split
+                constexpr bool SPLIT = decltype(SPLIT_)::value;
+                double beta = SPLIT ? beta0 : inv_p;
+                const int cl = SPLIT ? ctop_ : (Tw - 1) / kChunk;
+                const int clo = SPLIT ? clo_ : 0;
                 // per-chunk inputs (checkpoint, scale exponents, symbol pack) through a 4-deep register
                 // ring: chunk c - 4's are loaded as soon as chunk c is done with its slot; emissions
                 // through a 2-deep one; unrolled by 4 so no slot is copied (see the forward)
@@ -830,6 +947,18 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
                 double f_hi = 0.0, fu_hi = 0.0;  // scaled emissions at o_{8c+8} (from chunk c+1)
                 Em e_hi{};                       // PT: product pair at o_{8c+8} ...
                 int s_hi = 0;                    // ... and that step's scale exponent
+                if (SPLIT && cl < (Tw - 1) / kChunk) {  // a lower range: step 8 cl + 8 is chunk cl + 1's first
+                    const uint4 pn = loadpack(cl + 1);
+                    const int sn = exp_of(spw[(long long)(cl + 1) * U], 0);  // k = 0: always a scale step
+                    if constexpr (PT) {
+                        e_hi = ld_em(pn, 0);
+                        s_hi = sn;
+                    } else {
+                        const double *r = brow(pn, 0);
+                        f_hi = pow2_scale(r[0], sn);
+                        if constexpr (LR) fu_hi = pow2_scale(r[1], sn);
+                    }
+                }
                 auto chunk = [&](int c, const Ld &cur, const double (&zst)[ZF ? kChunk : 1], const uint4 &pkn, const Em (&bv)[kChunk],
                                  const double (&bu)[kChunk], Em (&bvn)[kChunk], double (&bun)[kChunk],
                                  const unsigned (&hac)[kChunk], unsigned (&han)[kChunk], auto MASK_) {
@@ -990,31 +1119,31 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
                         // ragged wave: masked while a trip holds some lane's last frames, then the
                         // chunks with t <= Tmin - 2 for every lane (c <= (Tmin - 9) / 8) unmasked
                         const int cr = Tmin >= kChunk + 1 ? (Tmin - kChunk - 1) / kChunk : -1;
-                        for (; c >= 3 && c > cr; c -= 4) {
+                        for (; c >= clo + 3 && c > cr; c -= 4) {
                             body(c, I1{}, Mk{});
                             body(c - 1, I2{}, Mk{});
                             body(c - 2, I3{}, Mk{});
                             body(c - 3, I0{}, Mk{});
                         }
                         using U0 = std::false_type;
-                        for (; c >= 3; c -= 4) {
+                        for (; c >= clo + 3; c -= 4) {
                             body(c, I1{}, U0{});
                             body(c - 1, I2{}, U0{});
                             body(c - 2, I3{}, U0{});
                             body(c - 3, I0{}, U0{});
                         }
                     }
-                    for (; c >= 3; c -= 4) {
+                    for (; c >= clo + 3; c -= 4) {
                         body(c, I1{}, Mk{});
                         body(c - 1, I2{}, Mk{});
                         body(c - 2, I3{}, Mk{});
                         body(c - 3, I0{}, Mk{});
                     }
-                    if (c >= 0) {
+                    if (c >= clo) {
                         body(c, I1{}, Mk{});
-                        if (c >= 1) {
+                        if (c - 1 >= clo) {
                             body(c - 1, I2{}, Mk{});
-                            if (c >= 2) body(c - 2, I3{}, Mk{});
+                            if (c - 2 >= clo) body(c - 2, I3{}, Mk{});
                         }
                     }
                 } else {  // global histogram atomics (skipped for zero gamma): the compact loop
@@ -1026,12 +1155,19 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
                     }
                 }
             };
-            if (safe) {
-                if (full) backward(std::true_type{}, std::false_type{});
-                else backward(std::true_type{}, std::true_type{});
+            using NoSp = std::false_type;
+            if (SPLITOK && spl) {  // full waves only: A the chunks from the top down to hc, B hc - 1 down to 0
+                const int ctop = brole ? hc - 1 : (Tw - 1) / kChunk;
+                const int clo = brole ? 0 : hc;
+                const double beta0 = brole ? beta_h : inv_p;
+                if (safe) backward(std::true_type{}, std::false_type{}, std::true_type{}, ctop, clo, beta0);
+                else backward(std::false_type{}, std::false_type{}, std::true_type{}, ctop, clo, beta0);
+            } else if (safe) {
+                if (full) backward(std::true_type{}, std::false_type{}, NoSp{}, 0, 0, 0.0);
+                else backward(std::true_type{}, std::true_type{}, NoSp{}, 0, 0, 0.0);
             } else {
-                if (full) backward(std::false_type{}, std::false_type{});
-                else backward(std::false_type{}, std::true_type{});
+                if (full) backward(std::false_type{}, std::false_type{}, NoSp{}, 0, 0, 0.0);
+                else backward(std::false_type{}, std::true_type{}, NoSp{}, 0, 0, 0.0);
             }
             if constexpr (PT) gex = S[0] + S[1];
             gall += gex;
@@ -1046,6 +1182,8 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
                 }
             }
         }
+    } else if (split_wg) {  // no sequence group here: the split barrier still counts every wave
+        __syncthreads();
     }
 
     __syncthreads();

@@ -366,3 +366,38 @@ def test_spread_extra_waves_ragged_vs_oracle(oracle_mt, monkeypatch, xact, topol
                           ("gamma_den_all", "log_gden_all"), ("B_num", "log_bnum")):
             np.testing.assert_allclose(g[key], np.exp(getattr(s, lkey)), rtol=STAT_RTOL, atol=1e-300, err_msg=key)
     assert np.isclose(StatsLayout.lse_of_pairs(g["ll_pairs"]), oracle_mt.lse(s.logP), rtol=1e-12)
+
+
+@pytest.mark.parametrize("split", ["0", "1"])
+@pytest.mark.parametrize("T,topology,safe", [(203, "left_to_right", False), (203, "dense", False), (9, "left_to_right", False),
+                                             (64, "left_to_right", True), (96, "dense", True)])
+def test_split_extra_waves_vs_oracle(oracle_mt, monkeypatch, split, T, topology, safe):
+    """Split extra waves (HMMBW_SPLIT_EXTRA, estep_small_body "split"): 10,000 equal-length sequences put a
+    second wave on 226 SIMDs; with the split each such group's backward is cut at chunk nch / 2 and its idle
+    partner wave runs the lower half from its own beta pre-sweep, rescaled into the forward's scaling.
+    Odd T (a partial top chunk), the two-chunk minimum (T = 9), per-step (safe) scaling, both topologies:
+    2 EM iterations and every statistic against the oracle (hmm_training.py:351-514)."""
+    from hmm_training_amd.engine import BaumWelchEngine
+    monkeypatch.setenv("HMMBW_SPLIT_EXTRA", split)
+    R, N, K, iters = 10_000, 8, 256, 2
+    sym = _symbols(R, T, N, K, "U", 71 + T)
+    off = np.arange(R + 1, dtype=np.int64) * T
+    pi, A, B = _params(N, K, topology, 71)
+    ref = oracle_mt.hmm_training(off, sym.astype(np.int64), N, K, 0.0, iters, pi, A, B)
+    with BaumWelchEngine(N, K, topology=topology, safe_scaling=safe) as eng:
+        eng.set_observations(offsets=off, symbols=sym)
+        eng.set_params(pi, A, B)
+        eng.reset(0.0, iters)
+        eng.enqueue_iterations(iters)
+        st, recs = eng.status(0, iters)
+        np.testing.assert_allclose([L for L, _ in recs], ref.trace_L, rtol=LL_RTOL)
+        np.testing.assert_allclose(eng.loglik(), ref.logP, rtol=LL_RTOL)
+        p_out, A_out, B_out = eng.params(normalise=True)
+        p_cur, A_cur, B_cur = eng.params(normalise=False)
+        g, ll, _ = statistics_pass(eng, N, K, R)
+    assert_params(A_out, ref.A, "A")
+    assert_params(B_out, ref.B, "B")
+    assert_params(p_out, ref.pi, "pi")
+    s = oracle_mt.estep_logstats(off, sym.astype(np.int64), N, K, p_cur, A_cur, B_cur)
+    np.testing.assert_allclose(ll, s.logP, rtol=LL_RTOL)
+    assert_stats(g, s, R, T)

@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--topology", default="left_to_right")
     ap.add_argument("--no-merge", action="store_true")
     ap.add_argument("--iters", type=int, default=6)
+    ap.add_argument("--prewarm", type=int, default=3000, help="untimed iterations first (GPU clock ramp)")
     ap.add_argument("--kwaves", type=int, default=0, help="kernel waves to read (default: R / sequences per wave)")
     ap.add_argument("--lib", default=None, help="prebuilt diagnostics library (default hmm_training_amd/libhmmbw_phase.so)")
     a = ap.parse_args()
@@ -56,6 +57,10 @@ def run_one(a, R, torch, BaumWelchEngine, default_initial_params, out_dir):
     eng = BaumWelchEngine(N, K, topology=a.topology, merge_mstep=not a.no_merge)
     eng.set_observations(offsets=np.arange(R + 1, dtype=np.int64) * T, symbols=sym)
     eng.set_params(pi, A, Bm)
+    if a.prewarm > 0:
+        eng.reset(0.0, a.prewarm + 1)
+        eng.enqueue_iterations(a.prewarm)
+        torch.cuda.synchronize()
     eng.reset(0.0, a.iters + 1)
     eng.enqueue_iterations(a.iters)
     torch.cuda.synchronize()
