@@ -411,6 +411,9 @@ constexpr int kTabPad = HMMBW_TAB_PAD;
 #ifndef HMMBW_ZFULL
 #define HMMBW_ZFULL 1
 #endif
+#ifndef HMMBW_SPLIT_LR  // split extra waves in the left-to-right kernels too (A/B builds)
+#define HMMBW_SPLIT_LR 0
+#endif
 constexpr int kHistOff = kTabPad ? 40960 : 32768;
 __host__ __device__ constexpr bool lds_tables_fit(int K, int GP) { return (size_t)K * GP * 16 <= (size_t)kHistOff; }
 __host__ __device__ constexpr size_t lds_table_bytes(int K, int GP) { return (size_t)kHistOff + (size_t)K * GP * 16; }
@@ -460,7 +463,7 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
     // split extra waves possible in this instantiation: dense E-step with LDS tables and atomic statistics
     // (dense cfg3 69.4 -> 64.3 us; left-to-right 34.0 -> 35.6 us, and its code alone costs registers:
     // profiles/r5/split_extra_ab.txt)
-    constexpr bool SPLITOK = !LR && LDSTAB && !FWD_ONLY && !DET;
+    constexpr bool SPLITOK = (!LR || HMMBW_SPLIT_LR) && LDSTAB && !FWD_ONLY && !DET;
     extern __shared__ __attribute__((aligned(256))) double smem[];  // 256-B aligned whatever the static LDS (ds_read_b128 rows)
     __shared__ double sPA[G + N * N];  // pi (zero-padded to G) and A of this iteration
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
