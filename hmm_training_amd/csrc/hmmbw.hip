@@ -472,7 +472,8 @@ struct hmmbw_ctx {
     long long nblocks = 0;
     long long nfull = 0;          // small kernels: workgroups with 4 active waves (then xact-wave ones)
     int xact = 4;
-    int prio = 2;                 // wave priority of the small kernels (EArgs::prio); HMMBW_PRIO overrides it
+    int prio = -1;                // wave priority of the small kernels (EArgs::prio): -1 auto (left-to-right 2,
+                                  // dense 0: profiles/r5/spread_knobs.txt); HMMBW_PRIO overrides it
     int split_extra = 1;          // EArgs::split_extra (HMMBW_SPLIT_EXTRA=0 turns it off)
     uint16_t *d_sym = nullptr;
     long long *d_wsym = nullptr, *d_wckoff = nullptr, *d_wspoff = nullptr;
@@ -644,7 +645,7 @@ EArgs make_eargs(hmmbw_ctx *c) {
     a.off_bnum = c->off_bnum();
     a.nfull = c->nfull;
     a.xact = c->xact;
-    a.prio = c->prio;
+    a.prio = c->prio >= 0 ? c->prio : (c->topo == HMMBW_TOPOLOGY_LEFT_TO_RIGHT ? 2 : 0);
     a.split_extra = c->split_extra;
     return a;
 }
@@ -1331,6 +1332,9 @@ int hmmbw_set_observations(hmmbw_ctx *c, const int64_t *offsets, const int32_t *
             const long long extra = nwaves - (long long)ncu * wpb;
             const char *xe = std::getenv("HMMBW_XACT");
             int xa = extra <= 2LL * ncu ? 2 : wpb;
+            // dense (as requested before the observations) with the split extra waves: one group per extra
+            // workgroup while they fit one per CU (cfg3 dense 63.5 -> 62.2 us, profiles/r5/spread_knobs.txt)
+            if (c->topo_req == HMMBW_TOPOLOGY_DENSE && c->split_extra && extra <= ncu) xa = 1;
             if (xe) xa = std::max(1, std::min(wpb, std::atoi(xe)));
             if (xa < wpb && (extra + xa - 1) / xa <= ncu) {
                 nfull = ncu;
