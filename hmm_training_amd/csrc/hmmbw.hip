@@ -1323,6 +1323,9 @@ int hmmbw_set_observations(hmmbw_ctx *c, const int64_t *offsets, const int32_t *
     // 6 waves instead of 8.  cfg3 (1,250 waves): 38.2 -> 36.5 us per iteration; xact = 1 (a prologue
     // and histogram flush per extra wave) and 3 measured no better.  HMMBW_XACT
     // overrides it (diagnostics: 1..4, 4 = every workgroup full).
+    // A/B switches (read before the map, which depends on the split)
+    if (const char *pe = std::getenv("HMMBW_PRIO")) c->prio = std::atoi(pe);
+    if (const char *se = std::getenv("HMMBW_SPLIT_EXTRA")) c->split_extra = std::atoi(se) != 0;
     long long nfull = nblocks;
     int xact = wpb;
     if (!c->wide && !c->det) {
@@ -1431,8 +1434,6 @@ int hmmbw_set_observations(hmmbw_ctx *c, const int64_t *offsets, const int32_t *
     c->nblocks = nblocks;
     c->nfull = nfull;
     c->xact = xact;
-    if (const char *pe = std::getenv("HMMBW_PRIO")) c->prio = std::atoi(pe);
-    if (const char *se = std::getenv("HMMBW_SPLIT_EXTRA")) c->split_extra = std::atoi(se) != 0;
     c->has_obs = true;
     if (int rc2 = ensure_wq(c)) return rc2;
     return ensure_zf(c);
