@@ -28,7 +28,10 @@ SMALL_N = range(1, 17)
 
 def units():
     """(source, extra defines, object stem) of every translation unit."""
-    u = [(SRC, [], "hmmbw"), (os.path.join(CSRC, "estep_wide_inst.hip"), [], "estep_wide"),
+    # the wide (fp64 MFMA) kernels with LLVM's memory-clause scheduler: fewer spills in k_estep_mfma<4>
+    # (31 VGPRs against 38) and the cfg5 shard's E-step 1,447 against 1,477 us (profiles/r5/ab_sched_strategy.txt)
+    wide_flags = ["-mllvm", "-amdgpu-sched-strategy=max-memory-clause"]
+    u = [(SRC, [], "hmmbw"), (os.path.join(CSRC, "estep_wide_inst.hip"), wide_flags, "estep_wide"),
          (os.path.join(CSRC, "vq.hip"), [], "vq")]
     u += [(os.path.join(CSRC, "estep_small_inst.hip"), [f"-DHMMBW_INST_N={n}"], f"estep_small_n{n}")
           for n in SMALL_N]
