@@ -330,6 +330,12 @@ def roofline_bounds(R, T, N, kern_s, traffic, issue, estep_s=None, lmap=None):
                             "unit": "fraction of the busiest SIMD's VALU issue cycles", "frac": t_simd / kern_s,
                             "t_bound_us": 1e6 * t_simd, "valu_per_wave": nw, "valu_fp64_per_wave": n64w,
                             "waves_on_busiest_simd": wmax, "source": issue["source"], "provenance": issue["provenance"]}
+        if lmap and lmap.get("split_extra"):
+            # The map counts sequence-group waves.  A split group runs on two waves (A: forward + upper backward,
+            # B: beta pre-sweep + lower backward), each on its own SIMD, so the busiest SIMD's second wave holds
+            # only part of a group: charging it a whole group makes this an upper bound on that SIMD's load.
+            out["simd_valu"]["note"] = "upper bound: a split extra group's A or B wave charged as a whole group"
+            out["split_extra_groups"] = waves - min(lmap["full_workgroups"], lmap["workgroups"]) * lmap["waves_per_workgroup"]
     if issue and kern_s > 0 and N <= 16 and issue.get("lds_array_cycles"):
         # SQ_LDS_IDX_ACTIVE = every LDS-array cycle of the launch, bank-conflict cycles included, per active wave
         t_lds = wcu * issue["lds_array_cycles"] / waves / t_clock
@@ -688,6 +694,12 @@ def main(argv=None):
     issue = find_issue(cfg_key)
     estep_s = (est_ms / est_n / 1000.0) if est_n else None
     lmap = eng.launch_map()
+    # Dense split extra waves (hmmbw.hip set_observations / estep_small_body SPLITOK): each extra
+    # workgroup's idle waves carry the B half of one sequence group; equal-length groups of nch >= 2 chunks.
+    lmap["split_extra"] = bool(topo == "dense" and N <= 16 and not args.deterministic and T >= 9
+                               and int(os.environ.get("HMMBW_SPLIT_EXTRA", "1") or 0) != 0
+                               and lmap.get("extra_waves") and lmap["full_workgroups"] < lmap["workgroups"]
+                               and 2 * lmap["extra_waves"] <= lmap["waves_per_workgroup"])
     bounds = roofline_bounds(R, T, N, kern_s, traffic, issue, estep_s, lmap)
     # The roofline (the task's contract and SURVEY §8(d)): ALGORITHMIC work per launch over the kernel's
     # average launch duration against the peak of the bounding resource.  Small kernels: HBM, B_u = 24T +
