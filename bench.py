@@ -294,8 +294,9 @@ def roofline_bounds(R, T, N, kern_s, traffic, issue, estep_s=None, lmap=None):
     waves, wmax, wcu = engine_waves(R, N, lmap)
     t_clock = CLOCK_MAX_GHZ * 1e9
     out = {"waves_per_launch": waves, "waves_on_busiest_simd": wmax, "waves_on_busiest_cu": wcu,
-           "wave_map": ("engine launch map (HMMBW_INFO_*), workgroup i on CU i mod 256" if lmap and not lmap.get("work_queue")
-                        else "pigeonhole (no launch map)"),
+           "wave_map": ("engine launch map (HMMBW_INFO_*), workgroup i on CU i mod 256"
+                        + (" (joined: extra workgroup i runs as waves 4.. of workgroup i, the same CU)" if lmap.get("joined") else "")
+                        if lmap and not lmap.get("work_queue") else "pigeonhole (no launch map)"),
            "clock_ghz": CLOCK_MAX_GHZ}
     if traffic and kern_s > 0:
         ach = traffic[0] / kern_s / 1e9
@@ -694,12 +695,7 @@ def main(argv=None):
     issue = find_issue(cfg_key)
     estep_s = (est_ms / est_n / 1000.0) if est_n else None
     lmap = eng.launch_map()
-    # Dense split extra waves (hmmbw.hip set_observations / estep_small_body SPLITOK): each extra
-    # workgroup's idle waves carry the B half of one sequence group; equal-length groups of nch >= 2 chunks.
-    lmap["split_extra"] = bool(topo == "dense" and N <= 16 and not args.deterministic and T >= 9
-                               and int(os.environ.get("HMMBW_SPLIT_EXTRA", "1") or 0) != 0
-                               and lmap.get("extra_waves") and lmap["full_workgroups"] < lmap["workgroups"]
-                               and 2 * lmap["extra_waves"] <= lmap["waves_per_workgroup"])
+    small_kernel = "k_estep_join" if lmap.get("joined") else "k_estep_small"  # the joined map's 8-wave kernel
     bounds = roofline_bounds(R, T, N, kern_s, traffic, issue, estep_s, lmap)
     # The roofline (the task's contract and SURVEY §8(d)): ALGORITHMIC work per launch over the kernel's
     # average launch duration against the peak of the bounding resource.  Small kernels: HBM, B_u = 24T +
@@ -722,11 +718,11 @@ def main(argv=None):
         model = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
                  "units_per_launch": R,
                  "work_per_unit": f"{bu} bytes (SURVEY §8(d): 24 T + 16 N T + 8 per sequence)",
-                 "kernel": "k_estep_small", "kernel_ms": 1e3 * kern_s}
+                 "kernel": small_kernel, "kernel_ms": 1e3 * kern_s}
     roof = {"bound": model["bound"], "achieved": model["achieved"], "peak": model["peak"], "unit": model["unit"],
             "frac": model["frac"], "traffic": traffic[0] if traffic else None,
             "model": model,
-            "kernel": "k_estep_mfma + k_bnum_gather (E-step)" if wide else "k_estep_small (E-step)",
+            "kernel": "k_estep_mfma + k_bnum_gather (E-step)" if wide else f"{small_kernel} (E-step)",
             "kernel_ms": kern_s * 1000.0, "kernel_time_source": kern_src,
             "binding": ({"resource": bounds["binding"], **{k: b[k] for k in ("achieved", "peak", "unit", "frac")},
                          "t_bound_us": b.get("t_bound_us"), "provenance": b.get("provenance")} if b else None),

@@ -59,6 +59,8 @@ INFO_WAVES_PER_WORKGROUP = 104
 INFO_FULL_WORKGROUPS = 105
 INFO_EXTRA_WAVES = 106
 INFO_PEER_CHUNKS = 107
+INFO_JOINED = 108
+INFO_SPLIT_EXTRA = 109
 ALLREDUCE = {"rccl": 0, "peer": 1}
 
 

@@ -16,7 +16,7 @@ Kernels small_kernels_n<HMMBW_INST_N>(bool lr, bool ldstab) {
         if (ldstab)
             return Kernels{k_estep_small<N, G, true, true, false>, k_estep_small<N, G, true, true, true>,
                            k_estep_small_group<N, G, true, true, false>, k_estep_small_group<N, G, true, true, true>,
-                           k_estep_small<N, G, true, true, false, true>};
+                           k_estep_small<N, G, true, true, false, true>, k_estep_join<N, G>};
         return Kernels{k_estep_small<N, G, true, false, false>, k_estep_small<N, G, true, false, true>};
     }
     if (ldstab)

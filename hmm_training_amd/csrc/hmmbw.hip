@@ -475,6 +475,8 @@ struct hmmbw_ctx {
     int prio = -1;                // wave priority of the small kernels (EArgs::prio): -1 auto (left-to-right 2,
                                   // dense 0: profiles/r5/spread_knobs.txt); HMMBW_PRIO overrides it
     int split_extra = 1;          // EArgs::split_extra (HMMBW_SPLIT_EXTRA=0 turns it off)
+    int join = 1;                 // left-to-right E-step on the joined spread map (k_estep_join; HMMBW_JOIN=0 off)
+    long long last_nll = 0;       // per-workgroup log-likelihood pairs written by the last E-step launch
     uint16_t *d_sym = nullptr;
     long long *d_wsym = nullptr, *d_wckoff = nullptr, *d_wspoff = nullptr;
     int *d_wT = nullptr, *d_wfull = nullptr, *d_slen = nullptr, *d_sseq = nullptr;
@@ -745,6 +747,7 @@ struct Plan {
     unsigned grid = 0, block = kBlock;
     size_t lds = 0;
     bool flip = false;
+    long long nll = 0;  // per-workgroup log-likelihood pairs the launch writes (tiles on the wide work queue)
 };
 
 // E-step launch e accumulates into copies and llpart; it clears `zero` (zero_len doubles) and, when
@@ -789,8 +792,24 @@ int ensure_wq(hmmbw_ctx *c) {
     return HMMBW_OK;
 }
 
+// The left-to-right E-step runs the joined spread map (k_estep_join): every extra workgroup of the spread map
+// (at most one per CU) becomes waves 4.. of the full workgroup with its index, so each CU runs one 8-wave
+// workgroup: one M-step prologue, one set of LDS tables and one histogram flush instead of two on the CUs
+// that host an extra workgroup.  cfg3: 32.2 -> 30.9 us per iteration (profiles/r5/join_ab.txt).
+bool joined_map(const hmmbw_ctx *c) {
+    return c->join && !c->wide && !c->det && c->topo == HMMBW_TOPOLOGY_LEFT_TO_RIGHT && c->lds_tables() &&
+           c->nblocks > c->nfull && c->nblocks - c->nfull <= c->nfull && c->xact <= kBlock / kWave;
+}
+
+// The dense kernels' split extra waves run (estep_small_body SPLITOK, "split").
+bool split_extra_map(const hmmbw_ctx *c) {
+    return c->split_extra && !c->wide && !c->det && c->topo == HMMBW_TOPOLOGY_DENSE && c->lds_tables() &&
+           c->nblocks > c->nfull && 2 * c->xact <= kBlock / kWave;
+}
+
 int plan_estep(hmmbw_ctx *c, bool fwd_only, const IterState *state, double *copies, double *llpart, double *zero,
-               long long zero_len, bool merge, Plan *P, double *rank_ll = nullptr, int ncopies = 0) {
+               long long zero_len, bool merge, Plan *P, double *rank_ll = nullptr, int ncopies = 0,
+               bool allow_join = true) {
     Plan &p = *P;
     p = Plan{};
     EArgs &a = p.a;
@@ -805,6 +824,7 @@ int plan_estep(hmmbw_ctx *c, bool fwd_only, const IterState *state, double *copi
     a.done_ctr = c->d_ctr;
     const int wpb = kBlock / kWave;
     p.grid = (unsigned)c->nblocks;
+    p.nll = c->nblocks;
     if (c->wide) {
         // exchange images [2][2 NP][17] (+ the backward's masked-z images [2][NP][17]) and the per-block
         // reduction scratch (estep_mfma.hpp)
@@ -835,6 +855,14 @@ int plan_estep(hmmbw_ctx *c, bool fwd_only, const IterState *state, double *copi
             const int NV = (lr ? 2 : c->N) + 3;
             const size_t tabs = c->lds_table_doubles();
             p.lds = sizeof(double) * (tabs + (size_t)wpb * c->G * NV + 8);
+            // joined spread map: extra workgroup b's waves become waves 4.. of full workgroup b
+            if (!fwd_only && allow_join && joined_map(c) && ks.join_estep) {
+                p.fn = ks.join_estep;
+                p.grid = (unsigned)c->nfull;
+                p.nll = c->nfull;
+                p.block = 2 * kBlock;
+                p.lds = sizeof(double) * (tabs + (size_t)(2 * wpb) * c->G * NV + 8);
+            }
             if (HMMBW_ZFULL && !lr && !fwd_only) {  // dense: the forward stores every z_t (hmmbw_device.hpp)
                 if (int rc = ensure_zf(c)) return rc;
                 a.ckpt = c->d_zf;
@@ -871,6 +899,7 @@ int launch_estep(hmmbw_ctx *c, bool fwd_only, const IterState *state, double *co
         HIP_TRY(hipEventRecord(e0, c->stream));
     }
     if (int rc = launch_lds(p.fn, p.grid, p.lds, c->stream, a, p.block)) return rc;
+    if (!fwd_only) c->last_nll = p.nll;
     hipEvent_t em = nullptr;
     if (e0 && (c->wide || c->det)) {
         if (c->mid_free.empty()) {
@@ -1326,6 +1355,7 @@ int hmmbw_set_observations(hmmbw_ctx *c, const int64_t *offsets, const int32_t *
     // A/B switches (read before the map, which depends on the split)
     if (const char *pe = std::getenv("HMMBW_PRIO")) c->prio = std::atoi(pe);
     if (const char *se = std::getenv("HMMBW_SPLIT_EXTRA")) c->split_extra = std::atoi(se) != 0;
+    if (const char *je = std::getenv("HMMBW_JOIN")) c->join = std::atoi(je) != 0;
     long long nfull = nblocks;
     int xact = wpb;
     if (!c->wide && !c->det) {
@@ -1536,6 +1566,8 @@ int hmmbw_get_option(const hmmbw_ctx *c, int key, int64_t *value) {
         case HMMBW_INFO_FULL_WORKGROUPS: *value = c->wide ? c->nblocks : std::min(c->nfull, c->nblocks); return HMMBW_OK;
         case HMMBW_INFO_EXTRA_WAVES: *value = c->wide ? 0 : c->xact; return HMMBW_OK;
         case HMMBW_INFO_PEER_CHUNKS: *value = c->d_peer ? c->peer_nch : 0; return HMMBW_OK;
+        case HMMBW_INFO_JOINED: *value = c->has_obs && joined_map(c) ? 1 : 0; return HMMBW_OK;
+        case HMMBW_INFO_SPLIT_EXTRA: *value = c->has_obs && split_extra_map(c) ? 1 : 0; return HMMBW_OK;
         default: return fail(HMMBW_E_INVALID, "unknown option " + std::to_string(key));
     }
 }
@@ -1605,7 +1637,7 @@ int hmmbw_estep(hmmbw_ctx *c, double *stats_dev) {
     const long long n = c->copy_len();
     const unsigned grid = (unsigned)std::min<long long>((n + 255) / 256, 64);
     hipLaunchKernelGGL(k_reduce_local, dim3(grid), dim3(256), 0, c->stream, c->copies(0), c->det ? 1 : c->ncopies, n, llp,
-                       c->nblocks, stats_dev, c->off_ll(), c->world, c->rank, c->state());
+                       c->last_nll, stats_dev, c->off_ll(), c->world, c->rank, c->state());
     HIP_TRY(hipGetLastError());
     return HMMBW_OK;
 }
@@ -1959,7 +1991,7 @@ int hmmbw_iterate(hmmbw_ctx *c, int64_t n_iter) {
         p.src = c->copies(e);
         p.nsrc = c->det ? 1 : c->ncopies;
         p.ll = c->llpart(e);
-        p.nll = c->nblocks;
+        p.nll = c->last_nll;
         p.ext = nullptr;
         p.R = c->R;
         if (!c->can_merge())
@@ -2451,7 +2483,7 @@ int hmmbw_group_iterate(hmmbw_group *g, int64_t n_iter) {
                     const long long nz = (long long)c->ncopies * c->copy_len();
                     Plan &p = plans[(size_t)l * n + i];
                     if (int rc = plan_estep(c, false, c->state(), c->copies(e), c->llpart(e), c->copies(e + 1), nz,
-                                            true, &p))
+                                            true, &p, nullptr, 0, false))
                         return rc;
                     if (!p.gfn || p.gfn != plans[0].gfn || p.block != kBlock)
                         return fail(HMMBW_E_UNSUPPORTED, "group members need the same grouped kernel");

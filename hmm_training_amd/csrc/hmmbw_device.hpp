@@ -443,9 +443,14 @@ __device__ __forceinline__ void rank_ll_fold(const EArgs &a, long long nblk);
 // repeated runs are bitwise identical: gamma goes to per-position rows in HBM (summed per symbol in a
 // fixed order by k_bnum_gather, as on the wide path) instead of the LDS histogram, and each workgroup
 // writes its partial statistics with plain stores (summed over workgroups in order by k_det_reduce).
-template <int N, int G, bool LR, bool LDSTAB, bool FWD_ONLY, bool DET = false>
+// BLK = 2 kBlock (k_estep_join, left-to-right E-step): the spread map's extra workgroup bid runs as waves
+// 4.. of full workgroup bid (one 8-wave workgroup per CU), so each CU builds one set of LDS tables, runs
+// one M-step prologue and flushes one histogram.
+template <int N, int G, bool LR, bool LDSTAB, bool FWD_ONLY, bool DET = false, int BLK = kBlock>
 __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long bid, const long long nblk) {
     static_assert(!DET || (LDSTAB && !FWD_ONLY), "deterministic mode: E-step with LDS tables");
+    constexpr bool JOIN = BLK > kBlock;
+    static_assert(!JOIN || (BLK == 2 * kBlock && LR && LDSTAB && !FWD_ONLY && !DET), "joined map: left-to-right E-step");
     constexpr int U = kWave / G;
     // dense G = 8: xi on the 4x4x4 MFMA (xi_mfma8), two accumulators per lane in its D layout
     constexpr bool XM = !LR && G == 8 && !FWD_ONLY && HMMBW_XI_MFMA;
@@ -463,7 +468,7 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
     // split extra waves possible in this instantiation: dense E-step with LDS tables and atomic statistics
     // (dense cfg3 69.4 -> 64.3 us; left-to-right 34.0 -> 35.6 us, and its code alone costs registers:
     // profiles/r5/split_extra_ab.txt)
-    constexpr bool SPLITOK = (!LR || HMMBW_SPLIT_LR) && LDSTAB && !FWD_ONLY && !DET;
+    constexpr bool SPLITOK = (!LR || HMMBW_SPLIT_LR) && LDSTAB && !FWD_ONLY && !DET && !JOIN;
     extern __shared__ __attribute__((aligned(256))) double smem[];  // 256-B aligned whatever the static LDS (ds_read_b128 rows)
     __shared__ double sPA[G + N * N];  // pi (zero-padded to G) and A of this iteration
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -479,20 +484,21 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
     double *sRed = smem + (LDSTAB ? lds_table_bytes(K, GP) / 8 : 0);  // [waves][G][NV] + ll scratch
     bool merged = false;
     if constexpr (LDSTAB && !FWD_ONLY) merged = a.merged != 0;
-    const int wpb = blockDim.x >> 6;
-    const bool xblk = bid >= a.nfull;
+    const int wpb = JOIN ? kBlock / kWave : blockDim.x >> 6;  // waves of a full (sequence-group) workgroup
+    const bool xblk = JOIN ? wv >= wpb : bid >= a.nfull;     // this wave runs an extra group
     // split extra waves: in an extra workgroup with 2 xact <= 4 waves, wave wv in [xact, 2 xact) is the B
     // partner of wave wv - xact (same sequence group): it runs the lower half of the group's backward
     const bool split_wg = SPLITOK && xblk && a.split_extra != 0 && 2 * a.xact <= wpb;
     const bool brole = split_wg && wv >= a.xact && wv < 2 * a.xact;
     const int wvg = brole ? wv - a.xact : wv;
-    const long long wave = xblk ? a.nfull * wpb + (bid - a.nfull) * a.xact + wvg : bid * wpb + wv;
-    const bool wactive = !xblk || wv < a.xact || brole;
+    const long long wave = JOIN ? (xblk ? a.nfull * wpb + bid * a.xact + (wv - wpb) : bid * wpb + wv)
+                                : (xblk ? a.nfull * wpb + (bid - a.nfull) * a.xact + wvg : bid * wpb + wv);
+    const bool wactive = !xblk || (JOIN ? wv - wpb : wv) < a.xact || brole;
     if (merged) {
         // the previous iteration's M-step, computed redundantly by every workgroup straight into
         // its LDS tables (no separate M-step kernel, no parameter round trip through HBM)
         if constexpr (LDSTAB && !FWD_ONLY)
-            if (!merged_mstep<N, G, GP, PT>(a, sP, sH, sPA, bid)) return;  // done or stopped (:346)
+            if (!merged_mstep<N, G, GP, PT, BLK>(a, sP, sH, sPA, bid)) return;  // done or stopped (:346)
     } else {
         if (a.state != nullptr && a.state->done) return;  // converged: device-side no-op
         if (tid < G) sPA[tid] = tid < N ? a.pi[tid] : 0.0;
@@ -502,11 +508,11 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
             // 16 independent loads in flight per thread before the first LDS store
             constexpr int TB = 16;
             const int nt = K * GP;
-            for (int i0 = 0; i0 < nt; i0 += TB * kBlock) {
+            for (int i0 = 0; i0 < nt; i0 += TB * BLK) {
                 double x[TB];
 #pragma unroll
                 for (int q = 0; q < TB; ++q) {
-                    const int i = i0 + q * kBlock + tid;
+                    const int i = i0 + q * BLK + tid;
                     const int k = i / GP, c = i - k * GP;
                     const bool ok = i < nt && k < K && c < G;
                     x[q] = a.Bt[ok ? (size_t)k * G + c : 0];
@@ -514,7 +520,7 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
                 }
 #pragma unroll
                 for (int q = 0; q < TB; ++q) {
-                    const int i = i0 + q * kBlock + tid;
+                    const int i = i0 + q * BLK + tid;
                     if (i < nt) {
                         if constexpr (PT) {
                             const int c = i % GP;
@@ -1290,6 +1296,13 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
 template <int N, int G, bool LR, bool LDSTAB, bool FWD_ONLY, bool DET = false>
 __global__ void __launch_bounds__(kBlock, 2) k_estep_small(EArgs a) {  // 2 waves per SIMD (<= 256 VGPRs)
     estep_small_body<N, G, LR, LDSTAB, FWD_ONLY, DET>(a, blockIdx.x, gridDim.x);
+}
+
+// Joined spread map (left-to-right E-step with LDS tables): one 8-wave workgroup per CU, grid = nfull;
+// waves 4.. of workgroup b run extra workgroup b's xact sequence groups (estep_small_body, JOIN).
+template <int N, int G>
+__global__ void __launch_bounds__(2 * kBlock, 1) k_estep_join(EArgs a) {
+    estep_small_body<N, G, true, true, false, false, 2 * kBlock>(a, blockIdx.x, gridDim.x);
 }
 
 // Grouped launch: g.nm models of one shape (same N, topology and tables), model m owning workgroups

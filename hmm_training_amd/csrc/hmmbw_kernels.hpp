@@ -18,6 +18,7 @@ struct Kernels {
     KernelFn estep = nullptr, score = nullptr;
     GroupFn group_estep = nullptr, group_score = nullptr;  // grouped launches (LDS tables only)
     KernelFn det_estep = nullptr;                          // deterministic-reduction E-step (LDS tables, wide)
+    KernelFn join_estep = nullptr;                         // joined spread map (left-to-right, LDS tables)
 };
 
 // E-step and scorer kernels for N states (1 <= N <= 16), left-to-right or dense, with or without the

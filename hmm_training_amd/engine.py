@@ -278,13 +278,16 @@ class BaumWelchEngine:
 
     def launch_map(self) -> dict:
         """The E-step launch's wave map (HMMBW_INFO_*): active waves, workgroups, waves per workgroup, the
-        workgroups with every wave active and the active waves of each workgroup after them."""
-        from ._lib import (INFO_EXTRA_WAVES, INFO_FULL_WORKGROUPS, INFO_WAVES, INFO_WAVES_PER_WORKGROUP,
-                           INFO_WORKGROUPS)
+        workgroups with every wave active and the active waves of each workgroup after them; `joined`: the
+        extra workgroups run as waves 4.. of the full ones (one 8-wave workgroup per CU); `split_extra`: the
+        extra workgroups' idle waves run the lower backward half of their groups (dense)."""
+        from ._lib import (INFO_EXTRA_WAVES, INFO_FULL_WORKGROUPS, INFO_JOINED, INFO_SPLIT_EXTRA, INFO_WAVES,
+                           INFO_WAVES_PER_WORKGROUP, INFO_WORKGROUPS)
         return {"waves": self.get_option(INFO_WAVES), "workgroups": self.get_option(INFO_WORKGROUPS),
                 "waves_per_workgroup": self.get_option(INFO_WAVES_PER_WORKGROUP),
                 "full_workgroups": self.get_option(INFO_FULL_WORKGROUPS),
-                "extra_waves": self.get_option(INFO_EXTRA_WAVES), "work_queue": self.work_queue_active}
+                "extra_waves": self.get_option(INFO_EXTRA_WAVES), "work_queue": self.work_queue_active,
+                "joined": self.get_option(INFO_JOINED) == 1, "split_extra": self.get_option(INFO_SPLIT_EXTRA) == 1}
 
     def peer_chunks(self) -> int:
         """Chunks of the peer all-reduce payload (one flag per (rank, chunk) per iteration), 0 without a region."""

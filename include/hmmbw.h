@@ -287,7 +287,12 @@ int hmmbw_set_option(hmmbw_ctx *ctx, int key, int64_t value);
  *                              after these);
  * HMMBW_INFO_EXTRA_WAVES       active waves of each workgroup after the full ones;
  * HMMBW_INFO_PEER_CHUNKS       chunks of the peer all-reduce payload (each rank writes and polls one flag
- *                              per (rank, chunk) per iteration), 0 without a peer region.
+ *                              per (rank, chunk) per iteration), 0 without a peer region;
+ * HMMBW_INFO_JOINED            1 if the E-step runs the joined map (left-to-right): extra workgroup b's
+ *                              waves run as waves 4.. of full workgroup b, one 8-wave workgroup per CU, so
+ *                              HMMBW_INFO_FULL_WORKGROUPS workgroups are launched (HMMBW_JOIN=0 turns it off);
+ * HMMBW_INFO_SPLIT_EXTRA       1 if the extra workgroups' idle waves run the lower backward half of their
+ *                              sequence groups (dense split; HMMBW_SPLIT_EXTRA=0 turns it off).
  * (bench.py's roofline bounds price the busiest CU and SIMD from this map.) */
 #define HMMBW_INFO_WIDE_WQ_ACTIVE 101
 #define HMMBW_INFO_WAVES 102
@@ -296,6 +301,8 @@ int hmmbw_set_option(hmmbw_ctx *ctx, int key, int64_t value);
 #define HMMBW_INFO_FULL_WORKGROUPS 105
 #define HMMBW_INFO_EXTRA_WAVES 106
 #define HMMBW_INFO_PEER_CHUNKS 107
+#define HMMBW_INFO_JOINED 108
+#define HMMBW_INFO_SPLIT_EXTRA 109
 int hmmbw_get_option(const hmmbw_ctx *ctx, int key, int64_t *value);
 
 /* E-step kernel timing with HIP events on the context stream (for bench/roofline).  Returns the

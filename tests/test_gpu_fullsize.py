@@ -330,15 +330,21 @@ def test_cfg5_whole_iteration_vs_oracle(oracle_mt, cfg5_whole_gpu):
             np.testing.assert_array_equal(x, y)  # replicated: bitwise-identical on every rank
 
 
-@pytest.mark.parametrize("xact,topology", [(None, "left_to_right"), ("1", "left_to_right"), ("3", "left_to_right"),
-                                           (None, "dense")])
-def test_spread_extra_waves_ragged_vs_oracle(oracle_mt, monkeypatch, xact, topology):
+@pytest.mark.parametrize("xact,topology,join", [(None, "left_to_right", None), ("1", "left_to_right", None),
+                                                ("3", "left_to_right", None), ("4", "left_to_right", None),
+                                                (None, "left_to_right", "0"), ("1", "left_to_right", "0"),
+                                                (None, "dense", None)])
+def test_spread_extra_waves_ragged_vs_oracle(oracle_mt, monkeypatch, xact, topology, join):
     """More waves than SIMDs (9,000 ragged sequences = 1,125 waves on 1,024 SIMDs): one full workgroup
-    per CU, then workgroups of xact active waves (default 2; HMMBW_XACT forces 1 or 3), with inactive
-    waves in them; every statistic and the trained model against the oracle (hmm_training.py:351-514)."""
+    per CU, then workgroups of xact active waves (default 2; HMMBW_XACT forces 1, 3 or 4 = no spread map),
+    with inactive waves in them; left-to-right by default on the joined map (the extra workgroups' waves as
+    waves 4.. of the full ones, k_estep_join), HMMBW_JOIN=0 the separate workgroups; every statistic and
+    the trained model against the oracle (hmm_training.py:351-514)."""
     from hmm_training_amd.engine import BaumWelchEngine, StatsLayout, to_csr
     if xact is not None:
         monkeypatch.setenv("HMMBW_XACT", xact)
+    if join is not None:
+        monkeypatch.setenv("HMMBW_JOIN", join)
     rng = np.random.default_rng(9)
     R, N, K, iters = 9000, 8, 256, 3
     obs = [rng.integers(0, K, size=int(t)) for t in rng.integers(60, 160, size=R)]
@@ -348,6 +354,10 @@ def test_spread_extra_waves_ragged_vs_oracle(oracle_mt, monkeypatch, xact, topol
     with BaumWelchEngine(N, K, topology=topology) as eng:
         eng.set_observations(obs)
         eng.set_params(pi, A, B)
+        lm = eng.launch_map()
+        spread = xact != "4"
+        assert (lm["workgroups"] > lm["full_workgroups"]) == spread, lm
+        assert lm["joined"] == (spread and topology == "left_to_right" and join != "0"), lm
         eng.reset(0.0, iters)
         eng.enqueue_iterations(iters)
         st, recs = eng.status(0, iters)

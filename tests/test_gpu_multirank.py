@@ -182,6 +182,13 @@ def test_split_iteration_multirank_vs_oracle(hip, oracle_mt, N, K, topology, R, 
         assert_params(p2, ref.pi, f"pi rank {r}")
 
 
+def test_split_iteration_multirank_joined_map_vs_oracle(hip, oracle_mt):
+    """Ranks with more sequence groups than SIMDs (9,000 ragged sequences per rank, left-to-right): the
+    joined spread map (k_estep_join, 8-wave workgroups) on the fused multi-rank path, whose last workgroup
+    folds the pairs of the 256 launched workgroups; 2 ranks against the oracle on the unsharded data."""
+    test_split_iteration_multirank_vs_oracle(hip, oracle_mt, 8, 256, "left_to_right", 18_000, 160, 2)
+
+
 def test_split_iteration_multirank_work_queue_vs_oracle(hip, oracle_mt, monkeypatch):
     """The wide work-queue E-step (more tiles than CUs per rank, HMMBW_WIDE_WQ=1) on the fused
     multi-rank path: the last backward unit folds the ranks' log-likelihood pairs over every tile."""
