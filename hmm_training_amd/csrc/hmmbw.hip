@@ -1369,7 +1369,10 @@ int hmmbw_set_observations(hmmbw_ctx *c, const int64_t *offsets, const int32_t *
             // workgroup while they fit one per CU (cfg3 dense 63.5 -> 62.2 us, profiles/r5/spread_knobs.txt)
             if (c->topo_req == HMMBW_TOPOLOGY_DENSE && c->split_extra && extra <= ncu) xa = 1;
             if (xe) xa = std::max(1, std::min(wpb, std::atoi(xe)));
-            if (xa < wpb && (extra + xa - 1) / xa <= ncu) {
+            // left-to-right on the joined map: past 2 extra groups per CU they still join the full workgroups,
+            // up to 4 per CU (cfg4 shard, 12,500 sequences: 135 workgroups of 8 waves instead of 2 x 135 of 4)
+            const bool join4 = !xe && xa == wpb && c->join && c->topo_req != HMMBW_TOPOLOGY_DENSE;
+            if ((xa < wpb || join4) && (extra + xa - 1) / xa <= ncu) {
                 nfull = ncu;
                 xact = xa;
                 nblocks = nfull + (extra + xa - 1) / xa;
