@@ -32,7 +32,9 @@
 //   k_finalise  the reference's return-path normalisation (:524-541).
 #include <dlfcn.h>
 
+#include <algorithm>
 #include <atomic>
+#include <climits>
 #include <cstdlib>
 #include <map>
 #include <mutex>
@@ -258,6 +260,13 @@ __global__ void __launch_bounds__(kPeerThreads) k_peer_allreduce(const double *b
     (void)peer_reduce_chunk(sum, P, seq, state, timeout_ticks, blockIdx.x);
 }
 
+// System-scope release + acquire on every XCD's L2 (buffer_wbl2 sc0 sc1, buffer_inv sc0 sc1): the grid has
+// more workgroups than XCDs, so each XCD's L2 sees at least one.  Used around the life of an uncached /
+// fine-grained peer region (peer_region_alloc / _free, HMMBW_PEER_FLUSH).
+__global__ void k_l2_flush() {
+    if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "");
+}
+
 __global__ void k_init_state(IterState *st, double eps, long long max_it) {
     st->prev_L = -INFINITY;
     st->last_L = -INFINITY;
@@ -314,12 +323,65 @@ size_t cache_class(size_t bytes) {
     return c;
 }
 enum { kDevBlock = 0, kPinnedBlock = 1 };
+
+// Allocation ledger (HMMBW_DEBUG_ALLOC=1, diagnostics): every driver allocation the library holds, with the
+// blocks the cache has handed out; a new allocation that overlaps a held one, a block handed out twice and a
+// free of an unknown block are reported on stderr.
+struct Ledger {
+    std::mutex mu;
+    std::map<uintptr_t, std::pair<size_t, std::string>> held;  // start -> (bytes, what)
+    std::map<uintptr_t, int> out;                              // cached blocks handed out
+};
+bool ledger_on() {
+    static const bool on = std::getenv("HMMBW_DEBUG_ALLOC") && std::atoi(std::getenv("HMMBW_DEBUG_ALLOC")) != 0;
+    return on;
+}
+Ledger &ledger() {
+    static Ledger *l = new Ledger;
+    return *l;
+}
+void ledger_add(const void *p, size_t bytes, const char *what) {
+    if (!ledger_on() || !p) return;
+    Ledger &L = ledger();
+    std::lock_guard<std::mutex> lk(L.mu);
+    const uintptr_t a = (uintptr_t)p;
+    auto it = L.held.upper_bound(a);
+    if (it != L.held.end() && it->first < a + bytes)
+        fprintf(stderr, "HMMBW_DEBUG_ALLOC: %s [%#lx, +%zu) overlaps held %s [%#lx, +%zu)\n", what, (unsigned long)a, bytes,
+                it->second.second.c_str(), (unsigned long)it->first, it->second.first);
+    if (it != L.held.begin()) {
+        auto jt = std::prev(it);
+        if (jt->first + jt->second.first > a)
+            fprintf(stderr, "HMMBW_DEBUG_ALLOC: %s [%#lx, +%zu) overlaps held %s [%#lx, +%zu)\n", what, (unsigned long)a,
+                    bytes, jt->second.second.c_str(), (unsigned long)jt->first, jt->second.first);
+    }
+    L.held[a] = std::make_pair(bytes, std::string(what));
+}
+void ledger_remove(const void *p, const char *what) {
+    if (!ledger_on() || !p) return;
+    Ledger &L = ledger();
+    std::lock_guard<std::mutex> lk(L.mu);
+    if (!L.held.erase((uintptr_t)p)) fprintf(stderr, "HMMBW_DEBUG_ALLOC: %s of unknown %p\n", what, p);
+}
+void ledger_out(const void *p, bool take) {
+    if (!ledger_on() || !p) return;
+    Ledger &L = ledger();
+    std::lock_guard<std::mutex> lk(L.mu);
+    int &n = L.out[(uintptr_t)p];
+    n += take ? 1 : -1;
+    if (n > 1) fprintf(stderr, "HMMBW_DEBUG_ALLOC: cached block %p handed out twice\n", p);
+    if (n < 0) fprintf(stderr, "HMMBW_DEBUG_ALLOC: cached block %p freed twice\n", p);
+}
+
 hipError_t cached_alloc(void **p, size_t bytes, int kind) {
     int dev = 0;
     (void)hipGetDevice(&dev);
-    if (bytes > kCacheMaxBlock)
-        return kind == kDevBlock ? hipMalloc(p, bytes)
-                                 : hipHostMalloc(p, bytes, hipHostMallocMapped | hipHostMallocCoherent);
+    if (bytes > kCacheMaxBlock) {
+        const hipError_t e = kind == kDevBlock ? hipMalloc(p, bytes)
+                                               : hipHostMalloc(p, bytes, hipHostMallocMapped | hipHostMallocCoherent);
+        if (e == hipSuccess && kind == kDevBlock) ledger_add(*p, bytes, "hipMalloc (large)");
+        return e;
+    }
     const size_t cls = cache_class(bytes);
     BlockCache &bc = block_cache();
     {
@@ -329,6 +391,7 @@ hipError_t cached_alloc(void **p, size_t bytes, int kind) {
             *p = it->second.back();
             it->second.pop_back();
             bc.held[std::make_pair(dev, kind)] -= cls;
+            if (kind == kDevBlock) ledger_out(*p, true);
             return hipSuccess;
         }
     }
@@ -338,6 +401,10 @@ hipError_t cached_alloc(void **p, size_t bytes, int kind) {
         std::lock_guard<std::mutex> lk(bc.mu);
         bc.size_of[*p] = std::make_pair(kind, cls);
     }
+    if (e == hipSuccess && kind == kDevBlock) {
+        ledger_add(*p, cls, "hipMalloc (cached class)");
+        ledger_out(*p, true);
+    }
     return e;
 }
 void cached_free(void *p, int kind) {
@@ -345,6 +412,7 @@ void cached_free(void *p, int kind) {
     int dev = 0;
     (void)hipGetDevice(&dev);
     BlockCache &bc = block_cache();
+    if (kind == kDevBlock && bc.size_of.count(p)) ledger_out(p, false);
     {
         std::lock_guard<std::mutex> lk(bc.mu);
         auto it = bc.size_of.find(p);
@@ -359,8 +427,12 @@ void cached_free(void *p, int kind) {
             bc.size_of.erase(it);
         }
     }
-    if (kind == kDevBlock) (void)hipFree(p);
-    else (void)hipHostFree(p);
+    if (kind == kDevBlock) {
+        ledger_remove(p, "hipFree");
+        (void)hipFree(p);
+    } else {
+        (void)hipHostFree(p);
+    }
 }
 // Release every cached block (all devices); returns the bytes given back to the driver.
 size_t cache_trim() {
@@ -383,8 +455,12 @@ size_t cache_trim() {
     (void)hipGetDevice(&dev0);
     for (auto &t : out) {
         (void)hipSetDevice(std::get<0>(t));
-        if (std::get<1>(t) == kDevBlock) (void)hipFree(std::get<2>(t));
-        else (void)hipHostFree(std::get<2>(t));
+        if (std::get<1>(t) == kDevBlock) {
+            ledger_remove(std::get<2>(t), "hipFree (trim)");
+            (void)hipFree(std::get<2>(t));
+        } else {
+            (void)hipHostFree(std::get<2>(t));
+        }
     }
     (void)hipSetDevice(dev0);
     return bytes;
@@ -517,6 +593,8 @@ struct hmmbw_ctx {
     double *d_xsum = nullptr;     // the all-reduced sums the pending M-step reads (peer mode)
     int peer_world = 0;
     bool peer_on = false;
+    bool peer_revoked = false;
+    bool peer_special = false;    // the region is uncached / fine-grained (HMMBW_PEER_MEM)    // a region this context was attached to was freed by its owner
     std::vector<double *> peer_regions;
     std::vector<void *> peer_mapped;
     unsigned long long peer_seq = 0;
@@ -589,12 +667,73 @@ void sync_ctx(hmmbw_ctx *c) {
     else (void)hipDeviceSynchronize();
 }
 
+// wall-clock ticks of a bound in ms, saturated (a huge bound must not wrap to a negative count, which
+// would end every wait at once)
+long long ms_to_ticks(const hmmbw_ctx *c, long long ms) {
+    const long long khz = std::max(1LL, c->wall_khz);
+    if (ms <= 0) return 0;
+    return ms > LLONG_MAX / khz ? LLONG_MAX : ms * khz;
+}
+
+// In-process attachments (hmmbw_peer_attach): region -> the contexts whose peer_regions hold it.  A context
+// that frees its region detaches every context still attached to it, so a later push of theirs fails with
+// HMMBW_E_STATE instead of writing into memory the allocator may already have handed to another buffer.
+struct PeerLinks {
+    std::mutex mu;
+    std::map<const void *, std::vector<hmmbw_ctx *>> users;
+};
+PeerLinks &peer_links() {
+    static PeerLinks *p = new PeerLinks;  // never destroyed
+    return *p;
+}
+
 // drop the attached peer regions (closing the IPC mappings of other ranks' regions)
 void peer_detach(hmmbw_ctx *c) {
     for (void *p : c->peer_mapped) (void)hipIpcCloseMemHandle(p);
     c->peer_mapped.clear();
+    {
+        PeerLinks &pl = peer_links();
+        std::lock_guard<std::mutex> lk(pl.mu);
+        for (double *r : c->peer_regions) {
+            auto it = pl.users.find(r);
+            if (it == pl.users.end()) continue;
+            auto &v = it->second;
+            v.erase(std::remove(v.begin(), v.end(), c), v.end());
+            if (v.empty()) pl.users.erase(it);
+        }
+    }
     c->peer_regions.clear();
     c->peer_on = false;
+}
+
+std::string peer_off_msg(const hmmbw_ctx *c) {
+    return c->peer_revoked ? "peer all-reduce: a rank's region this context was attached to has been freed "
+                             "(its context was destroyed or re-sized its region); attach again"
+                           : "peer all-reduce selected but no regions attached (hmmbw_peer_open / _attach)";
+}
+
+// this context's region is about to be freed: detach every other context attached to it (in-process)
+void peer_revoke(hmmbw_ctx *c) {
+    if (!c->d_peer) return;
+    PeerLinks &pl = peer_links();
+    std::lock_guard<std::mutex> lk(pl.mu);
+    auto it = pl.users.find(c->d_peer);
+    if (it == pl.users.end()) return;
+    for (hmmbw_ctx *u : it->second) {
+        if (u == c) continue;
+        for (double *r : u->peer_regions) {  // u's other links go too: its exchange is broken as a whole
+            if (r == c->d_peer) continue;
+            auto jt = pl.users.find(r);
+            if (jt == pl.users.end()) continue;
+            auto &w = jt->second;
+            w.erase(std::remove(w.begin(), w.end(), u), w.end());
+            if (w.empty()) pl.users.erase(jt);
+        }
+        u->peer_regions.clear();
+        u->peer_on = false;
+        u->peer_revoked = true;
+    }
+    pl.users.erase(it);
 }
 
 void free_obs(hmmbw_ctx *c) {
@@ -840,7 +979,7 @@ int plan_estep(hmmbw_ctx *c, bool fwd_only, const IterState *state, double *copi
             a.wq = c->d_wq;
             a.wq_flag = c->d_wq + 2;
             a.wq_units = (int)c->nblocks;
-            a.wq_timeout_ticks = c->wq_timeout_ms * c->wall_khz;
+            a.wq_timeout_ticks = ms_to_ticks(c, c->wq_timeout_ms);
             if (!p.fn) return fail(HMMBW_E_UNSUPPORTED, "no wide work-queue kernel for N");
         }
     } else {
@@ -1048,63 +1187,63 @@ void resolve_topology(hmmbw_ctx *c) {
 }
 
 // Memory of the peer receive regions (HMMBW_PEER_MEM).  Other GPUs write payload and flags into a region
-// over xGMI while this GPU's reduce kernel polls it.  coarse (default): hipMalloc, as every multi-rank test
-// on one GPU ran it (in-process and two / four processes over IPC); the writers' stores are system-scope
-// write-through and the reader's loads system-scope.  uncached / finegrained: hipExtMallocWithFlags kinds
-// that no cache holds (as RCCL keeps its flags), taken from a per-device pool that is never returned to the
-// driver.  Measured (round 5): uncached regions allocated and freed per context corrupted the statistics of
-// later contexts in the same process and once ended in an illegal memory access (the suite alone passed),
-// consistent with the allocator handing freed uncached pages to buffers that take fp64 atomics; the pool keeps
-// such pages out of circulation.  Cross-GPU coherence of either kind is unmeasured here (no multi-GPU box).
-struct PeerPool {
-    std::mutex mu;
-    std::vector<std::tuple<int, unsigned, size_t, void *>> free;  // (device, flags, bytes, region)
-    std::map<void *, std::tuple<int, unsigned, size_t>> owned;
-};
-PeerPool &peer_pool() {
-    static PeerPool *p = new PeerPool;  // never destroyed (regions live for the process)
-    return *p;
+// over xGMI while this GPU's reduce kernel polls it.  coarse (default): hipMalloc; the writers' stores are
+// system-scope write-through and the reader's loads system-scope.  uncached / finegrained: the
+// hipExtMallocWithFlags kinds RCCL keeps its flags in.  Each region is allocated for its context and freed
+// with it.
+// Round 5 saw later contexts in one process get wrong statistics and once a MEMORY_APERTURE_VIOLATION after
+// many uncached regions had been freed.  Round 6 settled it (tools/uc_probe.py, profiles/r6/uc_probe.json,
+// tests/test_gpu_peer.py): fp64 and u32 atomics sum exactly on hipMalloc, uncached and fine-grained memory,
+// and the driver hands a freed region's addresses to the next ordinary allocations at once (flags 0, exact
+// atomics there too), so recycled pages do not break atomics.  What the signature fits is a write through
+// a stale peer pointer: an aperture violation is an address outside the GPU's range, what a kernel forms
+// from a per-wave offset buffer overwritten with doubles, and the freed region's addresses belong to the
+// next context's buffers.  In-process attachments (hmmbw_peer_attach) held raw pointers to other contexts'
+// regions with nothing to stop a push after the owner freed or re-sized its region; peer_revoke now detaches
+// every context attached to a region before the region is freed, and their next iteration fails with
+// HMMBW_E_STATE instead of writing (test_peer_push_after_a_peer_region_was_freed_is_an_error).  IPC
+// importers are safe by construction: their mapping keeps the exporter's pages alive until they close it.
+// Cross-GPU coherence of either kind over xGMI is unmeasured here (no multi-GPU box).
+// HMMBW_PEER_FLUSH (diagnostics, round 6): bit 0 flushes every L2 after allocating an uncached / fine-grained
+// region, bit 1 before freeing one
+int peer_flush_mode() {
+    const char *e = std::getenv("HMMBW_PEER_FLUSH");
+    return e ? std::atoi(e) : 0;
 }
 
 int peer_region_alloc(hmmbw_ctx *c, size_t b) {
+    c->peer_special = false;
     const char *pm = std::getenv("HMMBW_PEER_MEM");
     const std::string kind = pm ? pm : "coarse";
     if (kind == "coarse") {
         HIP_TRY(hipMalloc(reinterpret_cast<void **>(&c->d_peer), b));
+        ledger_add(c->d_peer, b, "peer region (coarse)");
         return HMMBW_OK;
     }
     if (kind != "uncached" && kind != "finegrained")
         return fail(HMMBW_E_INVALID, "HMMBW_PEER_MEM must be coarse, uncached or finegrained");
     const unsigned fl = kind == "finegrained" ? hipDeviceMallocFinegrained : hipDeviceMallocUncached;
-    PeerPool &pp = peer_pool();
-    std::lock_guard<std::mutex> lk(pp.mu);
-    for (size_t i = 0; i < pp.free.size(); ++i) {
-        auto &f = pp.free[i];
-        if (std::get<0>(f) == c->device && std::get<1>(f) == fl && std::get<2>(f) >= b) {
-            c->d_peer = static_cast<double *>(std::get<3>(f));
-            pp.free.erase(pp.free.begin() + (long)i);
-            return HMMBW_OK;
-        }
-    }
+    c->peer_special = true;
     void *p = nullptr;
     HIP_TRY(hipExtMallocWithFlags(&p, b, fl));
-    pp.owned[p] = std::make_tuple(c->device, fl, b);
+    ledger_add(p, b, kind == "finegrained" ? "peer region (fine-grained)" : "peer region (uncached)");
     c->d_peer = static_cast<double *>(p);
+    if (peer_flush_mode() & 1) {
+        hipLaunchKernelGGL(k_l2_flush, dim3(1024), dim3(64), 0, nullptr);
+        HIP_TRY(hipDeviceSynchronize());
+    }
     return HMMBW_OK;
 }
 
+// callers synchronise the device first (no launch of this context still writes the region)
 void peer_region_free(hmmbw_ctx *c) {
     if (!c->d_peer) return;
-    PeerPool &pp = peer_pool();
-    {
-        std::lock_guard<std::mutex> lk(pp.mu);
-        auto it = pp.owned.find(c->d_peer);
-        if (it != pp.owned.end()) {
-            pp.free.emplace_back(std::get<0>(it->second), std::get<1>(it->second), std::get<2>(it->second), c->d_peer);
-            c->d_peer = nullptr;
-            return;
-        }
+    peer_revoke(c);
+    if ((peer_flush_mode() & 2) && c->peer_special) {
+        hipLaunchKernelGGL(k_l2_flush, dim3(1024), dim3(64), 0, nullptr);
+        (void)hipDeviceSynchronize();
     }
+    ledger_remove(c->d_peer, "hipFree (peer region)");
     (void)hipFree(c->d_peer);
     c->d_peer = nullptr;
 }
@@ -1571,6 +1710,7 @@ int hmmbw_get_option(const hmmbw_ctx *c, int key, int64_t *value) {
         case HMMBW_INFO_PEER_CHUNKS: *value = c->d_peer ? c->peer_nch : 0; return HMMBW_OK;
         case HMMBW_INFO_JOINED: *value = c->has_obs && joined_map(c) ? 1 : 0; return HMMBW_OK;
         case HMMBW_INFO_SPLIT_EXTRA: *value = c->has_obs && split_extra_map(c) ? 1 : 0; return HMMBW_OK;
+        case HMMBW_INFO_PEER_SUM_PTR: *value = (int64_t)(intptr_t)c->d_xsum; return HMMBW_OK;
         default: return fail(HMMBW_E_INVALID, "unknown option " + std::to_string(key));
     }
 }
@@ -1616,6 +1756,10 @@ int hmmbw_reset_training(hmmbw_ctx *c, double epsilon, int64_t max_iterations) {
     // the work queue's counters and flags: a run stopped by a work-queue timeout leaves them armed (the
     // workgroups that start after the stop return at once and never reach the re-arm)
     if (c->d_wq) HIP_TRY(hipMemsetAsync(c->d_wq, 0, sizeof(unsigned) * ((size_t)c->nblocks + 2), c->stream));
+    // the fused multi-rank completion counter: workgroups that start after a device-side stop return
+    // before counting their log-likelihood pair, so a stopped launch leaves it part-way; the next run's
+    // last-workgroup fold must start from zero
+    HIP_TRY(hipMemsetAsync(c->d_ctr, 0, sizeof(int), c->stream));
     c->e_count = 0;
     c->armed = true;
     return HMMBW_OK;
@@ -1753,7 +1897,7 @@ static int peer_allreduce(hmmbw_ctx *c, double *buf, long long len) {
         return fail(HMMBW_E_STATE, "the all-reduce payload changed after hmmbw_peer_region (rank, world or options "
                                    "set after it): set up the peer regions again");
     c->peer_seq += 1;
-    const long long ticks = std::max(1LL, c->peer_timeout_ms) * c->wall_khz;
+    const long long ticks = ms_to_ticks(c, std::max(1LL, c->peer_timeout_ms));
     hipLaunchKernelGGL(k_peer_allreduce, dim3((unsigned)c->peer_nch, (unsigned)c->peer_world), dim3(kPeerThreads), 0,
                        c->stream, buf, c->d_xsum, peer_args(c), c->peer_seq, c->state(), ticks);
     HIP_TRY(hipGetLastError());
@@ -1763,7 +1907,7 @@ static int peer_allreduce(hmmbw_ctx *c, double *buf, long long len) {
 
 // the sums go to d_xsum, which becomes the pending M-step's source (mr_end)
 static int peer_reduce(hmmbw_ctx *c) {
-    const long long ticks = std::max(1LL, c->peer_timeout_ms) * c->wall_khz;
+    const long long ticks = ms_to_ticks(c, std::max(1LL, c->peer_timeout_ms));
     hipLaunchKernelGGL(k_peer_reduce, dim3((unsigned)c->peer_nch), dim3(kPeerThreads), 0, c->stream, c->d_xsum,
                        peer_args(c), c->peer_seq, c->state(), ticks);
     HIP_TRY(hipGetLastError());
@@ -1792,8 +1936,7 @@ int hmmbw_iterate_begin(hmmbw_ctx *c, int64_t n_seq_global, double **buf, int64_
     if (int rc = check_ready(c, true)) return rc;
     if (!buf || !n_doubles) return fail(HMMBW_E_INVALID, "null argument");
     if (n_seq_global < 0) return fail(HMMBW_E_INVALID, "negative sequence count");
-    if (c->ar_kind == HMMBW_ALLREDUCE_PEER && !c->peer_on)
-        return fail(HMMBW_E_STATE, "peer all-reduce selected but no regions attached (hmmbw_peer_open / _attach)");
+    if (c->ar_kind == HMMBW_ALLREDUCE_PEER && !c->peer_on) return fail(HMMBW_E_STATE, peer_off_msg(c));
     long long len = 0;
     if (int rc = mr_begin(c, n_seq_global, buf, &len)) return rc;
     if (c->peer_mode()) {  // the whole exchange is the engine's: push now, wait + sum in _end
@@ -1866,8 +2009,14 @@ static int peer_attach_impl(hmmbw_ctx *c, const std::vector<double *> &regions, 
     // a fresh exchange: clear this rank's slots and flags (every rank attaches before any iterates)
     HIP_TRY(hipMemset(c->d_peer, 0, c->peer_bytes));
     c->peer_regions = regions;
+    {
+        PeerLinks &pl = peer_links();
+        std::lock_guard<std::mutex> lk(pl.mu);
+        for (double *r : regions) pl.users[r].push_back(c);
+    }
     c->peer_seq = 0;
     c->peer_on = true;
+    c->peer_revoked = false;
     c->R_global = n_seq_global;  // the R of hmm_training.py:424 for hmmbw_iterate's loop
     return HMMBW_OK;
 }
@@ -1933,8 +2082,7 @@ int hmmbw_iterate(hmmbw_ctx *c, int64_t n_iter) {
         // multi-rank with the engine's own all-reduce: estep -> ncclAllReduce (this stream) or the peer
         // push / wait + sum -> mstep
         const bool peer = c->peer_mode();
-        if (c->ar_kind == HMMBW_ALLREDUCE_PEER && !peer)
-            return fail(HMMBW_E_STATE, "peer all-reduce selected but no regions attached (hmmbw_peer_open / _attach)");
+        if (c->ar_kind == HMMBW_ALLREDUCE_PEER && !peer) return fail(HMMBW_E_STATE, peer_off_msg(c));
         if (!peer && !c->comm)
             return fail(HMMBW_E_STATE, "multi-rank hmmbw_iterate needs hmmbw_comm_init or the peer all-reduce "
                                        "(or use hmmbw_iterate_begin / all-reduce / _end)");
@@ -2272,11 +2420,15 @@ int group_launch(hmmbw_group *g, const std::vector<Plan> &plans, int n_launch, b
     else HIP_TRY(hipEventCreateWithFlags(&sl.ev, hipEventDisableTiming));
     if (sl.cap < need) {
         if (sl.host) HIP_TRY(hipHostFree(sl.host));
-        if (sl.dev) HIP_TRY(hipFree(sl.dev));
+        if (sl.dev) {
+            ledger_remove(sl.dev, "hipFree (group args)");
+            HIP_TRY(hipFree(sl.dev));
+        }
         sl.host = sl.dev = nullptr;
         sl.cap = 0;
         HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&sl.host), need));
         HIP_TRY(hipMalloc(reinterpret_cast<void **>(&sl.dev), need));
+        ledger_add(sl.dev, need, "hipMalloc (group args)");
         sl.cap = need;
     }
     std::vector<unsigned> grid((size_t)n_launch, 0);
@@ -2454,7 +2606,10 @@ int hmmbw_group_destroy(hmmbw_group *g) {
             (void)hipEventDestroy(sl.ev);
         }
         if (sl.host) (void)hipHostFree(sl.host);
-        if (sl.dev) (void)hipFree(sl.dev);
+        if (sl.dev) {
+            ledger_remove(sl.dev, "hipFree (group args)");
+            (void)hipFree(sl.dev);
+        }
     }
     for (hipEvent_t e : g->ev_free) (void)hipEventDestroy(e);
     for (hipEvent_t e : g->ev_pending) (void)hipEventDestroy(e);

@@ -411,6 +411,9 @@ constexpr int kTabPad = HMMBW_TAB_PAD;
 #ifndef HMMBW_ZFULL
 #define HMMBW_ZFULL 1
 #endif
+#ifndef HMMBW_FLUSH_VMWAIT  // explicit vmcnt(0) before the histogram flush (round 6 A/B)
+#define HMMBW_FLUSH_VMWAIT 0
+#endif
 #ifndef HMMBW_SPLIT_LR  // split extra waves in the left-to-right kernels too (A/B builds)
 #define HMMBW_SPLIT_LR 0
 #endif
@@ -1196,6 +1199,13 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
     }
 
     __syncthreads();
+#if HMMBW_FLUSH_VMWAIT
+    // every load of the sweeps has landed long ago; saying so here keeps the compiler from waiting on the
+    // flush's global atomics below: at the join of the active and idle waves' paths it otherwise counts a
+    // ring load as possibly in flight and, before reusing its register, waits vmcnt(2), i.e. for the
+    // round trips of all but two of the histogram atomics issued after it
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+#endif
     // the B-numerator histogram's atomics first: their round trips overlap the reductions below
     if constexpr (!FWD_ONLY && !DET && LDSTAB) if (!(a.ablate & 1)) {
         // (round 4: starting each workgroup's pass at a different row, so that workgroups finishing together

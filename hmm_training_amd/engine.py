@@ -225,7 +225,34 @@ class BaumWelchEngine:
         buf = ctypes.create_string_buffer(b"".join(handles), 64 * len(handles))
         rc = self._lib.hmmbw_peer_open(self._ctx, buf, self.n_seq_global)
         # every rank must have attached (cleared its flags) before any rank pushes
-        return self._agree(rc == 0)
+        ok = self._agree(rc == 0)
+        if ok:  # collective, so the count (the key of close()'s rendezvous) agrees across the ranks
+            BaumWelchEngine._peer_setups += 1
+            self._peer_tag = BaumWelchEngine._peer_setups
+        return ok
+
+    _peer_setups = 0  # peer set-ups of this process (every rank runs the same sequence)
+
+    def _close_rendezvous(self, timeout_s: float) -> bool:
+        """Bounded meeting of the ranks before the receive region is freed: each rank counts itself in under
+        a key of the process group's store and waits (polling) until all have, or until timeout_s passes.
+        Unlike dist.barrier, a rank that never arrives (it died, or closes at another point) cannot hold the
+        others: they return False after the timeout and free their regions anyway (an IPC importer's mapping
+        keeps the memory it writes alive until it closes the handle)."""
+        import time
+        import torch.distributed as dist
+        store = dist.distributed_c10d._get_default_store()
+        key = f"hmmbw/peer_close/{self._peer_tag}"
+        world = dist.get_world_size(self._group)
+        store.add(key, 1)
+        t_end = time.monotonic() + timeout_s
+        delay = 1e-4
+        while store.add(key, 0) < world:
+            if time.monotonic() > t_end:
+                return False
+            time.sleep(delay)
+            delay = min(2 * delay, 0.01)
+        return True
 
     def _init_native_comm(self) -> bool:
         """Collective over the ranks: give the context its own RCCL communicator (hmmbw_comm_init), so
@@ -543,18 +570,22 @@ class BaumWelchEngine:
         check(self._lib.hmmbw_comm_payload(self._ctx, ctypes.byref(n)))
         return 8 * n.value
 
-    def close(self) -> None:
-        """Destroy the context.  With the peer all-reduce set up, every rank must call close() at the same
-        point (a collective): the ranks first meet at a barrier, so no rank frees its IPC-exported receive
-        region while another may still push into it (a rank whose wait timed out, or bench's fallback
-        after a failed leg)."""
+    def close(self, timeout_s: Optional[float] = None) -> None:
+        """Destroy the context.  With the peer all-reduce set up, every rank should call close() at the same
+        point: the ranks first meet (a bounded rendezvous on the process group's store, HMMBW_CLOSE_TIMEOUT_S,
+        default 60 s), so no rank frees its IPC-exported receive region while another may still push into it
+        (a rank whose wait timed out, or bench's fallback after a failed leg).  A rank that closes alone (an
+        exception path) is not held forever: after the timeout it frees its context anyway, and the ranks
+        still iterating then stop on their own bounded peer wait (HMMBW_E_TIMEOUT)."""
         if getattr(self, "_ctx", None):
             if getattr(self, "_peer_ok", False) and self.world_size > 1:
                 try:
                     import torch.distributed as dist
                     if dist.is_available() and dist.is_initialized():
                         torch.cuda.synchronize(self.device)  # this rank's pushes have landed
-                        dist.barrier(group=self._group)       # ... and every other rank's too
+                        if timeout_s is None:
+                            timeout_s = float(os.environ.get("HMMBW_CLOSE_TIMEOUT_S", "60"))
+                        self._close_rendezvous(timeout_s)    # ... and every other rank's too (bounded)
                 except Exception:  # noqa: BLE001 - a broken process group must not keep the context alive
                     pass
             self._lib.hmmbw_ctx_destroy(self._ctx)

@@ -280,8 +280,10 @@ int hmmbw_set_option(hmmbw_ctx *ctx, int key, int64_t value);
 /* The current value of an option above, or a read-only fact about the loaded observations' E-step launch:
  * HMMBW_INFO_WIDE_WQ_ACTIVE    1 if it runs on the wide work queue;
  * HMMBW_INFO_WAVES             active waves (small kernels: sequence-group waves; wide: tiles x NP/16);
- * HMMBW_INFO_WORKGROUPS        workgroups of the launch;
- * HMMBW_INFO_WAVES_PER_WORKGROUP  waves per workgroup;
+ * HMMBW_INFO_WORKGROUPS        workgroups of the spread map (full + extra); with HMMBW_INFO_JOINED = 1
+ *                              the launch itself is HMMBW_INFO_FULL_WORKGROUPS workgroups of twice
+ *                              HMMBW_INFO_WAVES_PER_WORKGROUP waves (see HMMBW_INFO_JOINED);
+ * HMMBW_INFO_WAVES_PER_WORKGROUP  waves per workgroup of the spread map;
  * HMMBW_INFO_FULL_WORKGROUPS   workgroups with every wave active (small kernels: the spread map puts the
  *                              waves past one per SIMD into workgroups of HMMBW_INFO_EXTRA_WAVES active waves
  *                              after these);
@@ -303,6 +305,9 @@ int hmmbw_set_option(hmmbw_ctx *ctx, int key, int64_t value);
 #define HMMBW_INFO_PEER_CHUNKS 107
 #define HMMBW_INFO_JOINED 108
 #define HMMBW_INFO_SPLIT_EXTRA 109
+/* diagnostics: device address of the peer all-reduce's sum buffer (the pending M-step's source), 0 without
+ * a peer region (tools/peer_diag.py) */
+#define HMMBW_INFO_PEER_SUM_PTR 110
 int hmmbw_get_option(const hmmbw_ctx *ctx, int key, int64_t *value);
 
 /* E-step kernel timing with HIP events on the context stream (for bench/roofline).  Returns the

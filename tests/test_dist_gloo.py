@@ -90,3 +90,40 @@ def test_sharded_stats_allreduce_equals_single_rank(world, case, tmp_path, oracl
     lp = oracle.estep_logstats(d["offsets"], d["symbols"], N, M, d["init_pi"], d["init_A"], d["init_B"]).logP
     assert np.isclose(StatsLayout.lse_of_pairs(red["ll_pairs"]), oracle.lse(lp), rtol=1e-13)
     assert np.isclose(d["trace_L"][0], oracle.lse(lp), rtol=1e-12)
+
+
+def _close_worker(rank, world, port, out_dir):
+    """Rank 1 never reaches close() (it exits early): rank 0's bounded rendezvous must return False after its
+    timeout instead of blocking; with both ranks present it returns True."""
+    import sys
+    import time
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        sys.path.insert(0, ROOT)
+        from hmm_training_amd.engine import BaumWelchEngine
+
+        class Fake:  # the rendezvous needs only the tag of the collective peer set-up and the group
+            _group = None
+        f = Fake()
+        f._peer_tag = 1
+        ok_all = BaumWelchEngine._close_rendezvous(f, 30.0)
+        f._peer_tag = 2
+        t0 = time.monotonic()
+        ok_alone = BaumWelchEngine._close_rendezvous(f, 0.5) if rank == 0 else None
+        dt = time.monotonic() - t0
+        np.save(os.path.join(out_dir, f"c{rank}.npy"), np.array([ok_all, bool(ok_alone), dt]))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_close_rendezvous_is_bounded(tmp_path):
+    """BaumWelchEngine.close() with the peer all-reduce meets the other ranks before freeing its
+    receive region; a rank that never arrives must not hold the others forever."""
+    mp.start_processes(_close_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True,
+                       start_method="spawn")
+    c0, c1 = np.load(tmp_path / "c0.npy"), np.load(tmp_path / "c1.npy")
+    assert c0[0] == 1 and c1[0] == 1      # both present: the rendezvous completes
+    assert c0[1] == 0 and 0.4 < c0[2] < 10  # rank 1 absent: rank 0 gives up after its 0.5 s bound

@@ -225,3 +225,68 @@ def test_split_iteration_call_order(hip):
         assert e._lib.hmmbw_iterate(e._ctx, 1) == HMMBW_E_STATE
         assert e._lib.hmmbw_reset_training(e._ctx, 1e-6, 3) == HMMBW_E_STATE
         e.iterate_end()
+
+
+def test_split_iteration_multirank_work_queue_timeout_then_oracle(hip, oracle_mt):
+    """a work-queue timeout on the fused multi-rank path leaves the completion counter (the
+    last-workgroup fold of the ranks' log-likelihood pairs) part-way, because workgroups that start after the
+    stop return before counting.  hmmbw_reset_training clears it: a first run with a 0-ms bound fails with
+    HMMBW_E_TIMEOUT on both ranks, then a second run of the same contexts with the default bound must match
+    the oracle on the unsharded data (hmm_training.py:351-514, :503 L over all sequences)."""
+    import torch
+    from hmm_training_amd._lib import HMMBW_E_TIMEOUT, HMMBWError
+    from hmm_training_amd.engine import BaumWelchEngine, shard_bounds, to_csr
+    from hmm_training_amd.hmm_training import default_initial_params
+    ncu = torch.cuda.get_device_properties(0).multi_processor_count
+    N, K, world, iters = 32, 64, 2, 3
+    R = 2 * (16 * ncu + 16 * 9 + 3)
+    rng = np.random.default_rng(91)
+    obs = [rng.integers(0, K, size=int(t)) for t in rng.integers(8, 24, size=R)]
+    pi, A, B = default_initial_params(N, K)
+    A = 0.5 * A + 0.5 * rng.dirichlet(np.ones(N), size=N)
+    B = rng.dirichlet(np.full(K, 2.0), size=N)
+    off, sym = to_csr(obs)
+    ref = oracle_mt.hmm_training(off, sym.astype(np.int64), N, K, 0.0, iters, pi, A, B)
+    bounds = shard_bounds([len(o) for o in obs], world)
+    engines = []
+    try:
+        for r, (lo, hi) in enumerate(bounds):
+            e = BaumWelchEngine(N, K, rank=r, world_size=world, topology="dense")
+            e.set_observations(obs[lo:hi], n_seq_global=R)
+            e.set_params(pi, A, B)
+            e.set_work_queue(1, timeout_ms=0)
+            assert e.work_queue_active
+            e.reset(0.0, iters)
+            engines.append(e)
+        for _ in range(iters):
+            bufs = [e.iterate_begin() for e in engines]
+            allreduce_in_process(hip, bufs)
+            for e in engines:
+                e.iterate_end()
+        for e in engines:
+            with pytest.raises(HMMBWError) as ei:
+                e.status()
+            assert ei.value.code == HMMBW_E_TIMEOUT
+        for e in engines:
+            e.set_params(pi, A, B)
+            e.set_work_queue(1, timeout_ms=10000)
+            e.reset(0.0, iters)
+        for _ in range(iters):
+            bufs = [e.iterate_begin() for e in engines]
+            allreduce_in_process(hip, bufs)
+            for e in engines:
+                e.iterate_end()
+        res = []
+        for e in engines:
+            st, recs = e.status(0, iters)
+            res.append((st, recs, e.params(normalise=True), e.loglik()))
+    finally:
+        for e in engines:
+            e.close()
+    np.testing.assert_allclose(np.concatenate([r[3] for r in res]), ref.logP, rtol=LL_RTOL)
+    for r, (st, recs, (p2, A2, B2), _) in enumerate(res):
+        assert st.iterations == iters and st.done
+        np.testing.assert_allclose([x for x, _ in recs], ref.trace_L, rtol=LL_RTOL)
+        assert_params(A2, ref.A, f"A rank {r}")
+        assert_params(B2, ref.B, f"B rank {r}")
+        assert_params(p2, ref.pi, f"pi rank {r}")

@@ -104,10 +104,17 @@ def run_world_peer(d, world, deterministic=False, iters=None):
 CASES = ["n8_k256_t200", "converge", "zero_prob_seq", "dense_n16", "n64_k1024_tiny", "n5_k256_cfg1"]
 
 
+PEER_MEM = ["coarse", "uncached"]
+
+
+@pytest.mark.parametrize("peer_mem", PEER_MEM)
 @pytest.mark.parametrize("deterministic", [False, True])
 @pytest.mark.parametrize("world", [2, 3, 8])
 @pytest.mark.parametrize("case", CASES)
-def test_peer_allreduce_in_process_matches_reference(case, world, deterministic):
+def test_peer_allreduce_in_process_matches_reference(case, world, deterministic, peer_mem, monkeypatch):
+    """Every rank on the reference's trace and parameters, with the receive regions in each memory kind
+    (HMMBW_PEER_MEM: coarse hipMalloc, or uncached as RCCL keeps its flags)."""
+    monkeypatch.setenv("HMMBW_PEER_MEM", peer_mem)
     d = load(case)
     bounds, out = run_world_peer(d, world, deterministic)
     for r, (st, recs, raw, (pi, A, B)) in enumerate(out):
@@ -240,6 +247,114 @@ def test_peer_wait_is_bounded():
             e.close()
 
 
+@pytest.mark.parametrize("peer_mem", PEER_MEM)
+def test_peer_push_after_a_peer_region_was_freed_is_an_error(peer_mem, monkeypatch):
+    """A context attached (in process) to another rank's region must not write into it after its owner freed
+    it: destroying rank 1 detaches rank 0, whose next iteration fails with HMMBW_E_STATE, and nothing is
+    pushed into the freed memory.  A fresh attach of rank 0 to a new rank 1 then trains on the reference's
+    trace again."""
+    from hmm_training_amd._lib import HMMBW_E_STATE, HMMBWError
+    from hmm_training_amd.engine import BaumWelchEngine
+    monkeypatch.setenv("HMMBW_PEER_MEM", peer_mem)
+    d = load("n8_k256_t200")
+    obs = observations(d)
+    N, M = int(d["N"]), int(d["M"])
+
+    def make(r):
+        e = BaumWelchEngine(N, M, rank=r, world_size=2)
+        e.set_observations(obs[r::2], n_seq_global=len(obs))
+        e.set_params(d["init_pi"], d["init_A"], d["init_B"])
+        e.reset(float(d["epsilon"]), int(d["max_iterations"]))
+        return e
+
+    e0, e1 = make(0), make(1)
+    try:
+        attach_in_process([e0, e1])
+        for e in (e0, e1):
+            e.iterate_begin()
+        for e in (e0, e1):
+            e.iterate_end()
+        e1.close()
+        with pytest.raises(HMMBWError) as ei:
+            e0.iterate_begin()
+        assert ei.value.code == HMMBW_E_STATE and "freed" in str(ei.value)
+        # re-attached to a new rank 1, rank 0 trains again from the start
+        e1 = make(1)
+        e0.set_params(d["init_pi"], d["init_A"], d["init_B"])
+        e0.reset(float(d["epsilon"]), int(d["max_iterations"]))
+        attach_in_process([e0, e1])
+        for _ in range(int(d["max_iterations"]) + 1):
+            for e in (e0, e1):
+                e.iterate_begin()
+            for e in (e0, e1):
+                e.iterate_end()
+        for e in (e0, e1):
+            st, recs = e.status(0, int(d["iterations"]))
+            assert st.done and st.iterations == int(d["iterations"])
+            np.testing.assert_allclose([x for x, _ in recs], d["trace_L"], rtol=LL_RTOL)
+            pi, A, B = e.params(normalise=True)
+            assert_params(A, d["out_A"], "A")
+            assert_params(B, d["out_B"], "B")
+    finally:
+        e0.close()
+        e1.close()
+
+
+def test_special_memory_atomics_and_reuse_after_free():
+    """Round 5's peer failure, mechanism (a) of the round-5 verdict, pinned by measurement (tests/native/uc_probe.hip,
+    built with the engine's -munsafe-fp-atomics): the fp64 and u32 atomics of the E-step's statistics flush sum
+    exactly on hipMalloc, uncached and fine-grained memory; and after an uncached or fine-grained region is
+    freed, the driver hands its addresses to the next ordinary hipMalloc blocks (allocation flags 0) whose
+    atomics are exact too.  So recycled pages do not corrupt fp64 atomics; what they do mean is that a write
+    through a stale pointer to a freed region lands in another live buffer, which peer_revoke rules out for
+    in-process attachments (test_peer_push_after_a_peer_region_was_freed_is_an_error)."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tests", "native"))
+    import build_probe
+    path = build_probe.OUT
+    assert os.path.exists(path), "tests/native/libucprobe.so missing: run __graft_entry__.build() first"
+    lib = ctypes.CDLL(path)
+    vp, sz = ctypes.c_void_p, ctypes.c_size_t
+    lib.ucp_alloc.argtypes = [ctypes.c_int, sz, ctypes.POINTER(vp)]
+    lib.ucp_free.argtypes = [vp]
+    lib.ucp_flags.argtypes = [vp, ctypes.POINTER(ctypes.c_uint)]
+    lib.ucp_atomics.argtypes = [vp, ctypes.c_longlong, ctypes.POINTER(ctypes.c_longlong),
+                                ctypes.POINTER(ctypes.c_longlong)]
+
+    def alloc(kind, n):
+        p = vp()
+        assert lib.ucp_alloc(kind, n, ctypes.byref(p)) == 0
+        return p.value
+
+    def atomics_exact(p, nbytes):
+        wf, wu = ctypes.c_longlong(), ctypes.c_longlong()
+        for nslots in (64, min(nbytes // 8, 4096)):  # contended and spread
+            assert lib.ucp_atomics(p, nslots, ctypes.byref(wf), ctypes.byref(wu)) == 0
+            if wf.value or wu.value:
+                return False
+        return True
+
+    for kind in (0, 1, 2):
+        p = alloc(kind, 1 << 20)
+        assert atomics_exact(p, 1 << 20), f"atomics wrong on memory kind {kind}"
+        lib.ucp_free(p)
+    reused = 0
+    for kind in (1, 2):
+        nbytes = 8 << 20
+        r = alloc(kind, nbytes)
+        lib.ucp_free(r)
+        blocks = [alloc(0, b) for b in (4 << 20, 1 << 20, 1 << 20, 65536)]
+        for p, b in zip(blocks, (4 << 20, 1 << 20, 1 << 20, 65536)):
+            f = ctypes.c_uint()
+            assert lib.ucp_flags(p, ctypes.byref(f)) == 0 and f.value == 0
+            reused += r <= p < r + nbytes
+            assert atomics_exact(p, b), "atomics wrong on a block allocated after a special region was freed"
+        for p in blocks:
+            lib.ucp_free(p)
+    # the probe's premise (profiles/r6/uc_probe.json): freed addresses come back at once
+    assert reused > 0, "no block reused a freed region's addresses (the allocator changed: revisit the note)"
+
+
 WORKER = r"""
 import json, os, sys
 import numpy as np
@@ -269,9 +384,10 @@ dist.destroy_process_group()
 """
 
 
+@pytest.mark.parametrize("peer_mem", PEER_MEM)
 @pytest.mark.parametrize("world,N,K,topology", [(2, 8, 256, "left_to_right"), (4, 8, 256, "left_to_right"),
                                                  (4, 24, 64, "dense")])
-def test_peer_allreduce_processes_ipc(oracle_mt, tmp_path, world, N, K, topology):
+def test_peer_allreduce_processes_ipc(oracle_mt, tmp_path, world, N, K, topology, peer_mem):
     """`world` rank processes on cuda:0: the IPC handles go through a gloo process group
     (all_gather_object), each rank maps every other rank's region with hipIpcOpenMemHandle (not
     hmmbw_peer_attach), and the engine's train() runs the native peer loop (one k_peer_allreduce per EM
@@ -299,7 +415,7 @@ def test_peer_allreduce_processes_ipc(oracle_mt, tmp_path, world, N, K, topology
     procs = []
     for r in range(world):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
-                   HMMBW_ROOT=ROOT, HMMBW_CASE=str(cpath), HMMBW_OUT=str(opath))
+                   HMMBW_ROOT=ROOT, HMMBW_CASE=str(cpath), HMMBW_OUT=str(opath), HMMBW_PEER_MEM=peer_mem)
         procs.append(subprocess.Popen([sys.executable, str(wpath)], env=env))
     try:
         rcs = [p.wait(timeout=240) for p in procs]
