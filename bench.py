@@ -46,6 +46,7 @@ from __future__ import annotations
 import argparse
 import glob
 import json
+import re
 import os
 import socket
 import subprocess
@@ -236,6 +237,7 @@ def find_issue(cfg_key):
                         "valu_fp64_per_launch": k.get("valu_fp64_insts"),
                         "mfma_busy_cycles": k.get("SQ_VALU_MFMA_BUSY_CYCLES"),
                         "lds_array_cycles": k.get("SQ_LDS_IDX_ACTIVE"),
+                        "lds_insts": k.get("SQ_INSTS_LDS"),
                         "waves_counted": k.get("SQ_WAVES"),
                         "clock_ghz_grbm_estimate": k.get("clock_ghz"), "source": os.path.relpath(path, ROOT),
                         "provenance": _provenance(k, path)}
@@ -243,6 +245,108 @@ def find_issue(cfg_key):
 
 
 CUS = SIMDS // 4
+
+
+def _newest_json(pattern, accept):
+    """The newest round's committed profile (profiles/rN/...) matching `pattern` whose content passes accept."""
+    best = None
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "**", pattern), recursive=True), key=_round_key):
+        try:
+            with open(path) as fh:
+                d = json.load(fh)
+        except Exception:
+            continue
+        if accept(d):
+            best = (d, path)
+    return best
+
+
+def find_chain():
+    """Measured dependent-chain cycles per step (tools/ubench_chain.hip, profiles/rN/ubench_chain.txt): the
+    forward step (DPP shift || multiply -> fma) and the backward beta step (multiply -> DPP shift -> fma), one
+    wave per SIMD and two."""
+    best = None
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "**", "ubench_chain.txt"), recursive=True), key=_round_key):
+        d, src = {}, None
+        with open(path) as fh:
+            for line in fh:
+                m = re.match(r"#\s*kernel_src_sha16\s+(\w+)", line)
+                if m:
+                    src = m.group(1)
+                m = re.match(r"(.+?)\s+waves\s+(\d+)\s+([\d.]+) cycles/step", line)
+                if m:
+                    d[(m.group(1).strip(), int(m.group(2)))] = float(m.group(3))
+        f1, b1 = d.get(("forward step (dpp+mul+fma)", 4)), d.get(("backward beta step (mul+dpp+fma)", 4))
+        if f1 and b1:
+            best = {"forward": f1, "backward": b1, "forward_2waves": d.get(("forward step (dpp+mul+fma)", 8)),
+                    "backward_2waves": d.get(("backward beta step (mul+dpp+fma)", 8)),
+                    "source": os.path.relpath(path, ROOT),
+                    "provenance": {"source": os.path.relpath(path, ROOT), "kernel_src_sha16": src,
+                                   "fresh": None, "note": "a microbenchmark of the step's instruction chain"}}
+    return best
+
+
+def roofline_latency(R, T, N, topo, kern_s, issue, lmap):
+    """Left-to-right headline (N <= 8 LDS tables): the dependent-chain bound and a per-phase model of the busiest
+    SIMD, read from committed profiles of the newest round:
+      phases   profiles/rN/phase_lr_*.json (tools/phase_times.py --json): the prologue (kernel start -> LDS tables
+               written) and the tail (backward done -> statistics flushed) of the waves on two-wave SIMDs, measured;
+      chain    profiles/rN/ubench_chain.txt: cycles per dependent forward / backward step;
+      isa      profiles/rN/isa_lr_steps.json (tools/isa_steps.py): instructions per step of the steady loops.
+    latency      = prologue + T x (chain_fwd + chain_bwd) / clock + tail: no schedule can beat the chains.
+    phase_model  = prologue + T x (max over {chain, busiest-SIMD VALU pipe, single-wave issue, busiest-CU LDS}
+                   per step, forward and backward) / clock + tail; its frac is the share of the kernel time that
+                   the chains, the VALU and the LDS jointly explain; the rest (`unexplained_us`) is itemised."""
+    if N > 8 or topo != "left_to_right" or kern_s <= 0:
+        return {}
+    ph = _newest_json("phase_lr_*.json", lambda d: d.get("T") == T and d.get("N") == N and d.get("R") == R
+                      and d.get("topology") == topo and "busy" in d.get("classes", {}))
+    isa = _newest_json("isa_lr_steps.json", lambda d: "forward" in d.get("loops", {}))
+    ch = find_chain()
+    if not (ph and isa and ch):
+        return {}
+    phd, php = ph
+    busy = phd["classes"]["busy"]
+    pro = busy["at_tables_us"]["p50"]
+    tail = busy["at_flush_us"]["p50"] - busy["at_backward_us"]["p50"]
+    f = CLOCK_MAX_GHZ * 1e3  # cycles per us
+    out = {}
+    lat = pro + T * (ch["forward"] + ch["backward"]) / f + tail
+    out["latency"] = {"achieved": lat / (kern_s * 1e6), "peak": 1.0, "unit": "fraction of the kernel time",
+                      "frac": lat / (kern_s * 1e6), "t_bound_us": lat,
+                      "parts_us": {"prologue": pro, "forward_chain": T * ch["forward"] / f,
+                                   "backward_chain": T * ch["backward"] / f, "tail": tail},
+                      "chain_cycles_per_step": {"forward": ch["forward"], "backward": ch["backward"]},
+                      "source": [os.path.relpath(php, ROOT), ch["source"]],
+                      "provenance": _provenance(phd, php)}
+    wmax = 2
+    wcu = engine_waves(R, N, lmap)[2] if lmap else 6
+    lds_cyc = (issue["lds_array_cycles"] / issue["lds_insts"]) if issue and issue.get("lds_insts") else 8.0
+    parts, steps = {}, {}
+    for nm in ("forward", "backward"):
+        c = isa[0]["loops"][nm]["per_step"]
+        n_all = sum(v for k, v in c.items() if k not in ("dpp", "lds_atomic"))
+        simd = wmax * (VALU_CYCLES * c.get("f64", 0) + VALU_CYCLES_32 * c.get("v32", 0))
+        single = 4.0 * n_all
+        lds = wcu * c.get("lds", 0) * lds_cyc
+        step = {"chain": ch[nm], "simd_valu_pipe": simd, "single_wave_issue": single, "cu_lds": lds}
+        steps[nm] = {**{k: round(v, 2) for k, v in step.items()}, "binding": max(step, key=step.get),
+                     "measured_busy": 1e3 * busy[("tables->forward_us" if nm == "forward" else "forward->backward_us")]["p50"]
+                     * CLOCK_MAX_GHZ / T}
+        parts[nm] = T * max(step.values()) / f
+    model = pro + parts["forward"] + parts["backward"] + tail
+    meas_end = busy["at_flush_us"]["p50"]
+    out["phase_model"] = {"achieved": model / (kern_s * 1e6), "peak": 1.0,
+                          "unit": "fraction of the kernel time the per-phase bounds explain", "frac": model / (kern_s * 1e6),
+                          "t_bound_us": model, "parts_us": {"prologue": pro, **parts, "tail": tail},
+                          "cycles_per_step": steps, "waves_on_busiest_simd": wmax, "waves_on_busiest_cu": wcu,
+                          "lds_cycles_per_instruction": lds_cyc,
+                          "unexplained_us": {"forward": busy["tables->forward_us"]["p50"] - parts["forward"],
+                                             "backward": busy["forward->backward_us"]["p50"] - parts["backward"],
+                                             "phase_build_span_vs_kernel": kern_s * 1e6 - meas_end},
+                          "source": [os.path.relpath(php, ROOT), os.path.relpath(isa[1], ROOT), ch["source"]],
+                          "provenance": _provenance(phd, php), "isa_provenance": _provenance(isa[0], isa[1])}
+    return out
 
 
 def engine_waves(R, N, lmap=None):
@@ -273,7 +377,7 @@ def engine_waves(R, N, lmap=None):
     return waves, -(-waves // SIMDS), -(-waves // CUS)
 
 
-def roofline_bounds(R, T, N, kern_s, traffic, issue, estep_s=None, lmap=None):
+def roofline_bounds(R, T, N, kern_s, traffic, issue, estep_s=None, lmap=None, topo=None):
     """Every ceiling that applies to the dominant launch, each as achieved / peak of ONE resource, so every
     frac is <= 1 when the measurement and the model are right; the binding bound is the largest frac.
 
@@ -344,6 +448,8 @@ def roofline_bounds(R, T, N, kern_s, traffic, issue, estep_s=None, lmap=None):
                          "frac": t_lds / kern_s, "t_bound_us": 1e6 * t_lds, "waves_on_busiest_cu": wcu,
                          "lds_cycles_per_wave": issue["lds_array_cycles"] / waves, "source": issue["source"],
                          "provenance": issue["provenance"]}
+    if topo is not None:
+        out.update(roofline_latency(R, T, N, topo, kern_s, issue, lmap))
     cands = {k: v for k, v in out.items() if isinstance(v, dict) and "frac" in v}
     out["binding"] = max(cands, key=lambda k: cands[k]["frac"]) if cands else None
     return out
@@ -696,7 +802,7 @@ def main(argv=None):
     estep_s = (est_ms / est_n / 1000.0) if est_n else None
     lmap = eng.launch_map()
     small_kernel = "k_estep_join" if lmap.get("joined") else "k_estep_small"  # the joined map's 8-wave kernel
-    bounds = roofline_bounds(R, T, N, kern_s, traffic, issue, estep_s, lmap)
+    bounds = roofline_bounds(R, T, N, kern_s, traffic, issue, estep_s, lmap, topo)
     # The roofline (the task's contract and SURVEY §8(d)): ALGORITHMIC work per launch over the kernel's
     # average launch duration against the peak of the bounding resource.  Small kernels: HBM, B_u = 24T +
     # 16NT + 8 bytes per sequence (a fixed conversion: it charges an alpha_hat round trip the

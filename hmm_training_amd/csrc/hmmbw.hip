@@ -260,11 +260,25 @@ __global__ void __launch_bounds__(kPeerThreads) k_peer_allreduce(const double *b
     (void)peer_reduce_chunk(sum, P, seq, state, timeout_ticks, blockIdx.x);
 }
 
-// System-scope release + acquire on every XCD's L2 (buffer_wbl2 sc0 sc1, buffer_inv sc0 sc1): the grid has
-// more workgroups than XCDs, so each XCD's L2 sees at least one.  Used around the life of an uncached /
-// fine-grained peer region (peer_region_alloc / _free, HMMBW_PEER_FLUSH).
-__global__ void k_l2_flush() {
-    if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "");
+// Validation of a new uncached / fine-grained peer region (peer_region_alloc): the pattern is written with the
+// push's system-scope stores, then read back with the reduce's system-scope loads and with ordinary loads;
+// every mismatch is counted.  Recycled pages can return stale data to kernel loads after a change of memory
+// type (see peer_region_alloc), which this catches before the region carries any statistics.
+__device__ __forceinline__ double region_pattern(long long i, unsigned seed) {
+    return (double)(((unsigned long long)i * 2654435761ull + seed) & 0xFFFFFFull) + 0.5;
+}
+__global__ void k_region_fill(double *r, long long n, unsigned seed) {
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+        __hip_atomic_store(r + i, region_pattern(i, seed), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__global__ void k_region_check(const double *r, long long n, unsigned seed, unsigned *bad) {
+    unsigned nb = 0;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+        const double want = region_pattern(i, seed);
+        nb += __hip_atomic_load(r + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != want;
+        nb += r[i] != want;
+    }
+    if (nb) atomicAdd(bad, nb);
 }
 
 __global__ void k_init_state(IterState *st, double eps, long long max_it) {
@@ -1187,28 +1201,55 @@ void resolve_topology(hmmbw_ctx *c) {
 }
 
 // Memory of the peer receive regions (HMMBW_PEER_MEM).  Other GPUs write payload and flags into a region
-// over xGMI while this GPU's reduce kernel polls it.  coarse (default): hipMalloc; the writers' stores are
-// system-scope write-through and the reader's loads system-scope.  uncached / finegrained: the
-// hipExtMallocWithFlags kinds RCCL keeps its flags in.  Each region is allocated for its context and freed
-// with it.
-// Round 5 saw later contexts in one process get wrong statistics and once a MEMORY_APERTURE_VIOLATION after
-// many uncached regions had been freed.  Round 6 settled it (tools/uc_probe.py, profiles/r6/uc_probe.json,
-// tests/test_gpu_peer.py): fp64 and u32 atomics sum exactly on hipMalloc, uncached and fine-grained memory,
-// and the driver hands a freed region's addresses to the next ordinary allocations at once (flags 0, exact
-// atomics there too), so recycled pages do not break atomics.  What the signature fits is a write through
-// a stale peer pointer: an aperture violation is an address outside the GPU's range, what a kernel forms
-// from a per-wave offset buffer overwritten with doubles, and the freed region's addresses belong to the
-// next context's buffers.  In-process attachments (hmmbw_peer_attach) held raw pointers to other contexts'
-// regions with nothing to stop a push after the owner freed or re-sized its region; peer_revoke now detaches
-// every context attached to a region before the region is freed, and their next iteration fails with
-// HMMBW_E_STATE instead of writing (test_peer_push_after_a_peer_region_was_freed_is_an_error).  IPC
-// importers are safe by construction: their mapping keeps the exporter's pages alive until they close it.
-// Cross-GPU coherence of either kind over xGMI is unmeasured here (no multi-GPU box).
-// HMMBW_PEER_FLUSH (diagnostics, round 6): bit 0 flushes every L2 after allocating an uncached / fine-grained
-// region, bit 1 before freeing one
-int peer_flush_mode() {
-    const char *e = std::getenv("HMMBW_PEER_FLUSH");
-    return e ? std::atoi(e) : 0;
+// over xGMI while this GPU's reduce kernel polls it.  coarse (default): hipMalloc, allocated and freed with
+// its context; the writers' stores are system-scope write-through and the reader's loads system-scope.
+// uncached / finegrained: the hipExtMallocWithFlags kinds RCCL keeps its flags in.
+// The cause of round 5's failures (wrong statistics in later contexts of one process, once a
+// MEMORY_APERTURE_VIOLATION), measured in round 6 (tools/uc_stale.py, profiles/r6/uc_stale.txt, tools/peer_diag.py,
+// profiles/r6/peer_diag.txt): the driver hands a freed ordinary block's addresses to the next uncached /
+// fine-grained allocation, and kernel loads from such a region (system-scope and ordinary alike) can then
+// return stale or foreign data while hipMemcpy reads what was written; an L2 write-back + invalidate between
+// the two lives does not clear it.  In the suite, the wide path's 2.2 MB region of rank 0 landed on the
+// addresses of the previous test's freed coarse region: every push landed (checked by hipMemcpy), but the
+// reduce kernel read zeros and 1e-20 (another context's B floor) for some entries, so the M-step's A and B
+// were wrong; the reverse transition (a freed special region's pages back as an ordinary buffer that kernels
+// read) fits the aperture violation, an address formed from offsets that came back as foreign data.
+// Fp64 atomics themselves sum exactly on every kind (tools/uc_probe.py).  Hence: special regions come from a
+// per-process pool and never go back to the driver (no special -> ordinary transition), and a new one is
+// validated with the push's stores and the reduce's loads before use (catches the ordinary -> special one;
+// a region that fails is quarantined, kept allocated and unused).  Separately, in-process attachments
+// (hmmbw_peer_attach) are revoked when their region is freed (peer_revoke), so no context can push through a
+// pointer to a freed region.  Cross-GPU coherence of either kind over xGMI is unmeasured here.
+struct PeerPool {
+    std::mutex mu;
+    std::vector<std::tuple<int, unsigned, size_t, void *>> free;  // (device, flags, bytes, region)
+    std::map<void *, std::tuple<int, unsigned, size_t>> owned;
+    std::vector<void *> quarantined;
+    long long validated = 0, rejected = 0;
+};
+PeerPool &peer_pool() {
+    static PeerPool *p = new PeerPool;  // never destroyed (its regions live for the process)
+    return *p;
+}
+
+// 0: the region reads back what was written; > 0: mismatching reads; < 0: HIP error
+long long validate_region(void *p, size_t bytes) {
+    const long long n = (long long)(bytes / sizeof(double));
+    unsigned *d_bad = nullptr;
+    if (hipMalloc(reinterpret_cast<void **>(&d_bad), sizeof(unsigned)) != hipSuccess) return -1;
+    unsigned bad = 0;
+    long long rc = 0;
+    for (unsigned seed = 1; seed <= 2 && rc == 0; ++seed) {
+        if (hipMemset(d_bad, 0, sizeof(unsigned)) != hipSuccess) { rc = -1; break; }
+        hipLaunchKernelGGL(k_region_fill, dim3(256), dim3(256), 0, nullptr, static_cast<double *>(p), n, seed);
+        if (hipDeviceSynchronize() != hipSuccess) { rc = -1; break; }
+        hipLaunchKernelGGL(k_region_check, dim3(256), dim3(256), 0, nullptr, static_cast<const double *>(p), n, seed, d_bad);
+        if (hipDeviceSynchronize() != hipSuccess ||
+            hipMemcpy(&bad, d_bad, sizeof(unsigned), hipMemcpyDeviceToHost) != hipSuccess) { rc = -1; break; }
+        rc = bad;
+    }
+    (void)hipFree(d_bad);
+    return rc;
 }
 
 int peer_region_alloc(hmmbw_ctx *c, size_t b) {
@@ -1224,24 +1265,56 @@ int peer_region_alloc(hmmbw_ctx *c, size_t b) {
         return fail(HMMBW_E_INVALID, "HMMBW_PEER_MEM must be coarse, uncached or finegrained");
     const unsigned fl = kind == "finegrained" ? hipDeviceMallocFinegrained : hipDeviceMallocUncached;
     c->peer_special = true;
-    void *p = nullptr;
-    HIP_TRY(hipExtMallocWithFlags(&p, b, fl));
-    ledger_add(p, b, kind == "finegrained" ? "peer region (fine-grained)" : "peer region (uncached)");
-    c->d_peer = static_cast<double *>(p);
-    if (peer_flush_mode() & 1) {
-        hipLaunchKernelGGL(k_l2_flush, dim3(1024), dim3(64), 0, nullptr);
-        HIP_TRY(hipDeviceSynchronize());
+    PeerPool &pp = peer_pool();
+    std::lock_guard<std::mutex> lk(pp.mu);
+    size_t best = SIZE_MAX;
+    long long bi = -1;
+    for (size_t i = 0; i < pp.free.size(); ++i) {  // smallest free region of this device and kind that fits
+        const auto &f = pp.free[i];
+        if (std::get<0>(f) == c->device && std::get<1>(f) == fl && std::get<2>(f) >= b && std::get<2>(f) < best) {
+            best = std::get<2>(f);
+            bi = (long long)i;
+        }
     }
-    return HMMBW_OK;
+    if (bi >= 0) {
+        c->d_peer = static_cast<double *>(std::get<3>(pp.free[(size_t)bi]));
+        pp.free.erase(pp.free.begin() + bi);
+        return HMMBW_OK;
+    }
+    // whole 2 MB units: in the probe only allocations past 2 MB that were not a multiple of it (2.25 MB, the
+    // wide path's region at world 2) read back wrong after an ordinary -> special reuse (uc_stale.txt)
+    const size_t nb = (b + (size_t(2) << 20) - 1) / (size_t(2) << 20) * (size_t(2) << 20);
+    for (int attempt = 0; attempt < 8; ++attempt) {
+        void *p = nullptr;
+        HIP_TRY(hipExtMallocWithFlags(&p, nb, fl));
+        ledger_add(p, nb, kind == "finegrained" ? "peer region (fine-grained)" : "peer region (uncached)");
+        const long long bad = validate_region(p, nb);
+        if (bad < 0) return fail(HMMBW_E_HIP, "validating a new peer region failed");
+        if (bad == 0) {
+            pp.validated += 1;
+            pp.owned[p] = std::make_tuple(c->device, fl, nb);
+            c->d_peer = static_cast<double *>(p);
+            return HMMBW_OK;
+        }
+        pp.rejected += 1;
+        pp.quarantined.push_back(p);  // stale pages: never used, never freed
+    }
+    return fail(HMMBW_E_HIP, "no " + kind + " peer region read back what was written (8 attempts quarantined): use "
+                "HMMBW_PEER_MEM=coarse");
 }
 
 // callers synchronise the device first (no launch of this context still writes the region)
 void peer_region_free(hmmbw_ctx *c) {
     if (!c->d_peer) return;
     peer_revoke(c);
-    if ((peer_flush_mode() & 2) && c->peer_special) {
-        hipLaunchKernelGGL(k_l2_flush, dim3(1024), dim3(64), 0, nullptr);
-        (void)hipDeviceSynchronize();
+    if (c->peer_special) {  // back to the pool, never to the driver
+        PeerPool &pp = peer_pool();
+        std::lock_guard<std::mutex> lk(pp.mu);
+        auto it = pp.owned.find(c->d_peer);
+        if (it != pp.owned.end())
+            pp.free.emplace_back(std::get<0>(it->second), std::get<1>(it->second), std::get<2>(it->second), c->d_peer);
+        c->d_peer = nullptr;
+        return;
     }
     ledger_remove(c->d_peer, "hipFree (peer region)");
     (void)hipFree(c->d_peer);
@@ -1711,6 +1784,13 @@ int hmmbw_get_option(const hmmbw_ctx *c, int key, int64_t *value) {
         case HMMBW_INFO_JOINED: *value = c->has_obs && joined_map(c) ? 1 : 0; return HMMBW_OK;
         case HMMBW_INFO_SPLIT_EXTRA: *value = c->has_obs && split_extra_map(c) ? 1 : 0; return HMMBW_OK;
         case HMMBW_INFO_PEER_SUM_PTR: *value = (int64_t)(intptr_t)c->d_xsum; return HMMBW_OK;
+        case HMMBW_INFO_PEER_REGIONS_VALIDATED:
+        case HMMBW_INFO_PEER_REGIONS_REJECTED: {
+            PeerPool &pp = peer_pool();
+            std::lock_guard<std::mutex> lk(pp.mu);
+            *value = key == HMMBW_INFO_PEER_REGIONS_VALIDATED ? pp.validated : pp.rejected;
+            return HMMBW_OK;
+        }
         default: return fail(HMMBW_E_INVALID, "unknown option " + std::to_string(key));
     }
 }

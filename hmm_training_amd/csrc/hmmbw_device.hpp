@@ -412,7 +412,7 @@ constexpr int kTabPad = HMMBW_TAB_PAD;
 #define HMMBW_ZFULL 1
 #endif
 #ifndef HMMBW_FLUSH_VMWAIT  // explicit vmcnt(0) before the histogram flush (round 6 A/B)
-#define HMMBW_FLUSH_VMWAIT 0
+#define HMMBW_FLUSH_VMWAIT 1
 #endif
 #ifndef HMMBW_SPLIT_LR  // split extra waves in the left-to-right kernels too (A/B builds)
 #define HMMBW_SPLIT_LR 0

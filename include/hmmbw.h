@@ -308,6 +308,10 @@ int hmmbw_set_option(hmmbw_ctx *ctx, int key, int64_t value);
 /* diagnostics: device address of the peer all-reduce's sum buffer (the pending M-step's source), 0 without
  * a peer region (tools/peer_diag.py) */
 #define HMMBW_INFO_PEER_SUM_PTR 110
+/* process-wide: uncached / fine-grained peer regions validated, and rejected (quarantined) because kernel
+ * loads did not read back what was written (see hmmbw.hip, peer_region_alloc) */
+#define HMMBW_INFO_PEER_REGIONS_VALIDATED 111
+#define HMMBW_INFO_PEER_REGIONS_REJECTED 112
 int hmmbw_get_option(const hmmbw_ctx *ctx, int key, int64_t *value);
 
 /* E-step kernel timing with HIP events on the context stream (for bench/roofline).  Returns the

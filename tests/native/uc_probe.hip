@@ -21,9 +21,97 @@ __global__ void k_add_u32(unsigned *p, long long nslots, int reps) {
     for (int r = 0; r < reps; ++r) atomicAdd(p + (g + r) % nslots, 1u);
 }
 
+__global__ void k_fill(double *p, long long n, double base) {  // ordinary (cached) stores
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+        p[i] = base + (double)i;
+}
+
+__global__ void k_sum_read(const double *p, long long n, double *out) {  // ordinary loads (lines into L2)
+    double s = 0.0;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+        s += p[i];
+    if (s == -1.0) out[0] = s;  // keeps the loads
+}
+
+__global__ void k_fill_sys(double *p, long long n, double base) {  // the peer push's system-scope stores
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+        __hip_atomic_store(p + i, base + (double)i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ void k_copy_sys(const double *p, long long n, double *out) {  // the peer reduce's system-scope loads
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+        out[i] = __hip_atomic_load(p + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ void k_copy_plain(const double *p, long long n, double *out) {  // ordinary loads
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+        out[i] = p[i];
+}
+
+__global__ void k_l2_flush() {  // system-scope release + acquire on every XCD
+    if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "");
+}
+
 }  // namespace
 
 extern "C" {
+
+// A page's life as ordinary (cached) memory, then as an uncached / fine-grained region (kind 1 / 2):
+//   1. c = hipMalloc(bytes), pattern A (1e6 + i) by a kernel, read back by a kernel (lines in the L2), free c
+//   2. u = the special allocation (same_va: u == c); hipMemset(u, 0); pattern B (2e6 + i) with system-scope stores
+//   3. read u with system-scope loads (sys) and with ordinary loads (plain) into a fresh buffer, and by hipMemcpy
+// counts[0..2] = elements != B for sys / plain / hipMemcpy; counts[3..5] = elements equal to pattern A;
+// counts[6] = same_va.  flush bit 0: an L2 write-back + invalidate kernel after step 1, bit 1 after step 2;
+// bit 2: a validation-like pass (kernel stores, then kernel loads) right after the allocation.
+int ucp_stale(int kind, size_t bytes, int flush, long long *counts) {
+    const long long n = (long long)(bytes / 8);
+    double *c = nullptr, *u = nullptr, *o = nullptr;
+    hipError_t e;
+    for (int i = 0; i < 7; ++i) counts[i] = 0;
+    if ((e = hipMalloc(reinterpret_cast<void **>(&o), bytes)) != hipSuccess) return (int)e;
+    if ((e = hipMalloc(reinterpret_cast<void **>(&c), bytes)) != hipSuccess) return (int)e;
+    hipLaunchKernelGGL(k_fill, dim3(1024), dim3(256), 0, 0, c, n, 1e6);
+    hipLaunchKernelGGL(k_sum_read, dim3(1024), dim3(256), 0, 0, c, n, o);
+    if ((e = hipDeviceSynchronize()) != hipSuccess) return (int)e;
+    if ((e = hipFree(c)) != hipSuccess) return (int)e;
+    if (flush & 1) {
+        hipLaunchKernelGGL(k_l2_flush, dim3(1024), dim3(64), 0, 0);
+        if ((e = hipDeviceSynchronize()) != hipSuccess) return (int)e;
+    }
+    if ((e = hipExtMallocWithFlags(reinterpret_cast<void **>(&u), bytes,
+                                   kind == 2 ? hipDeviceMallocFinegrained : hipDeviceMallocUncached)) != hipSuccess)
+        return (int)e;
+    counts[6] = (u == c) ? 1 : 0;
+    if (flush & 4) {  // the engine's validation pass before first use: kernel stores, then kernel loads
+        hipLaunchKernelGGL(k_fill_sys, dim3(1024), dim3(256), 0, 0, u, n, 3e6);
+        hipLaunchKernelGGL(k_copy_sys, dim3(1024), dim3(256), 0, 0, u, n, o);
+        hipLaunchKernelGGL(k_copy_plain, dim3(1024), dim3(256), 0, 0, u, n, o);
+        if ((e = hipDeviceSynchronize()) != hipSuccess) return (int)e;
+    }
+    if ((e = hipMemset(u, 0, bytes)) != hipSuccess) return (int)e;
+    if ((e = hipDeviceSynchronize()) != hipSuccess) return (int)e;
+    hipLaunchKernelGGL(k_fill_sys, dim3(1024), dim3(256), 0, 0, u, n, 2e6);
+    if ((e = hipDeviceSynchronize()) != hipSuccess) return (int)e;
+    if (flush & 2) {
+        hipLaunchKernelGGL(k_l2_flush, dim3(1024), dim3(64), 0, 0);
+        if ((e = hipDeviceSynchronize()) != hipSuccess) return (int)e;
+    }
+    std::vector<double> h((size_t)n);
+    for (int mode = 0; mode < 3; ++mode) {
+        if (mode == 0) hipLaunchKernelGGL(k_copy_sys, dim3(1024), dim3(256), 0, 0, u, n, o);
+        if (mode == 1) hipLaunchKernelGGL(k_copy_plain, dim3(1024), dim3(256), 0, 0, u, n, o);
+        if ((e = hipDeviceSynchronize()) != hipSuccess) return (int)e;
+        if ((e = hipMemcpy(h.data(), mode < 2 ? o : u, bytes, hipMemcpyDeviceToHost)) != hipSuccess) return (int)e;
+        for (long long i = 0; i < n; ++i) {
+            counts[mode] += h[(size_t)i] != 2e6 + (double)i;
+            counts[3 + mode] += h[(size_t)i] == 1e6 + (double)i;
+        }
+    }
+    (void)hipFree(u);
+    (void)hipFree(o);
+    return 0;
+}
+
 
 // kind 0 hipMalloc, 1 hipExtMallocWithFlags(uncached), 2 hipExtMallocWithFlags(fine-grained)
 int ucp_alloc(int kind, size_t bytes, void **out) {

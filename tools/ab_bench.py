@@ -1,7 +1,8 @@
 """On-box A/B of library variants through bench.py (pre-warmed, HIP-event GPU time per EM iteration),
 interleaved in rounds so that every variant sees the same box and clocks.
 
-    python tools/ab_bench.py --libs libhmmbw.so,libhmmbw_x.so --cases lr,dense,cfg4,t8 [--rounds 2] [--steps 200]
+    python tools/ab_bench.py --libs libhmmbw.so,libhmmbw_x.so,libhmmbw.so:HMMBW_XACT=1 --cases lr,dense,cfg4,t8 [--rounds 2]
+(';' separates library specs when one carries several settings: --libs 'libhmmbw.so;libhmmbw.so:A=1,B=2')
 
 cases: lr (cfg3 left-to-right), lrH (cfg3 skewed symbols), dense (cfg3 dense), cfg4 (the 12,500 shard),
 t8 (T = 8 at 8,192 sequences: the fixed cost per launch), cfg5 (the wide shard, 6,250 x 400).
@@ -24,8 +25,13 @@ CASES = {
 }
 
 
-def run(lib, case, steps):
+def run(spec, case, steps):
+    """spec: a library file name, optionally with environment settings: libhmmbw.so:HMMBW_XACT=1,HMMBW_JOIN=0"""
+    lib, _, envs = spec.partition(":")
     env = dict(os.environ, HMMBW_LIB=os.path.join(ROOT, "hmm_training_amd", lib))
+    for kv in filter(None, envs.split(",")):
+        k, _, v = kv.partition("=")
+        env[k] = v
     st = steps if case != "cfg5" else max(10, steps // 20)
     cmd = [sys.executable, "-u", os.path.join(ROOT, "bench.py"), "--no-cpu-baseline", "--no-synced",
            "--steps", str(st), "--warmup", "5", *CASES[case]]
@@ -46,7 +52,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--steps", type=int, default=200)
     a = ap.parse_args()
-    libs = a.libs.split(",")
+    libs = a.libs.split(";") if ";" in a.libs else a.libs.split(",")
     res = {}
     for r in range(a.rounds):
         for case in a.cases.split(","):

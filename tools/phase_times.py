@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--prewarm", type=int, default=3000, help="untimed iterations first (GPU clock ramp)")
     ap.add_argument("--kwaves", type=int, default=0, help="kernel waves to read (default: R / sequences per wave)")
     ap.add_argument("--lib", default=None, help="prebuilt diagnostics library (default hmm_training_amd/libhmmbw_phase.so)")
+    ap.add_argument("--json", default=None, help="write the per-class phase summary (busy / lone SIMDs) here")
     a = ap.parse_args()
     out_dir = os.path.join(ROOT, "gpurun_out", "phase")
     os.makedirs(out_dir, exist_ok=True)
@@ -94,6 +95,8 @@ def run_one(a, R, torch, BaumWelchEngine, default_initial_params, out_dir):
             r = us(t[:, k] - t0)
             print(f"at {nm:<12s} rel-start  min {r.min():7.2f}  p50 {np.median(r):7.2f}  max {r.max():7.2f} us")
     np.save(os.path.join(out_dir, "phase_nomerge.npy" if a.no_merge else "phase_merge.npy"), t)
+    if a.json:
+        write_json(a, R, eng, l, us)
     # per-chunk shader-clock durations (forward: chunk c -> c+1; backward: chunk c -> c-1)
     ck = np.zeros((nw_pad, 2, 64), dtype=np.uint64)
     l.hmmbw_debug_chunk_times.argtypes = [ctypes.c_void_p, ctypes.c_int64]
@@ -110,6 +113,61 @@ def run_one(a, R, torch, BaumWelchEngine, default_initial_params, out_dir):
           + " ".join(f"{np.median(fwd[:, c]):.0f}" for c in range(min(fwd.shape[1], 12))))
     print(f"backward chunk cycles: p50 {np.median(bwd):.0f}  mean {bwd.mean():.0f}  max {bwd.max():.0f}")
     print(f"shader clock estimate: {np.median(span_clk / np.maximum(span_us * (nch - 1) / nch, 1e-9)) / 1e3:.2f} GHz")
+
+
+def write_json(a, R, eng, l, us):
+    """Phase durations by SIMD class on the engine's launch map (bench.py's phase model reads this): `busy` =
+    the waves on SIMDs that hold two sequence-group waves (joined map: full waves 0 .. xact-1 and extra waves
+    4 .. 3+xact of the workgroups that carry extra groups), `lone` = the other full waves.  Stamps are indexed
+    by (workgroup, wave) of the launched kernel: 8 waves per workgroup on the joined map."""
+    import json
+    import time
+    sys.path.insert(0, ROOT)
+    import bench
+    m = eng.launch_map()
+    joined = bool(m.get("joined"))
+    wpw = 8 if joined else m["waves_per_workgroup"]
+    nwg = m["full_workgroups"] if joined else m["workgroups"]
+    xact = m["extra_waves"] or 4
+    nx_groups = m["waves"] - m["full_workgroups"] * 4
+    nx_wg = -(-nx_groups // xact) if nx_groups > 0 else 0
+    n = ((nwg * wpw + 3) // 4) * 4
+    buf = np.zeros((n, 16), dtype=np.uint64)
+    assert l.hmmbw_debug_phase_times(buf.ctypes.data, n) == 0
+    t = buf[:nwg * wpw].astype(np.int64)
+    t0 = t[t[:, 0] > 0, 0].min()
+    busy, lone = [], []
+    for b in range(nwg):
+        for wv in range(wpw):
+            idx = b * wpw + wv
+            if joined:
+                if b < nx_wg and (wv < xact or 4 <= wv < 4 + xact):
+                    busy.append(idx)
+                elif wv < 4:
+                    lone.append(idx)
+            elif wv < 4:
+                lone.append(idx)
+    out = {"tool": "tools/phase_times.py --json", "R": R, "T": a.T, "N": a.N, "K": a.K, "topology": a.topology,
+           "launch_map": m, "kernel_src_sha16": bench.kernel_source_hash(),
+           "collected_utc": time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime()),
+           "span_us": float(us(t[:, 5].max() - t0)), "classes": {}}
+    names = ["start", "tables", "forward", "backward", "ll", "flush"]
+    for cls, ids in (("busy", busy), ("lone", lone)):
+        if not ids:
+            continue
+        tt = t[ids]
+        tt = tt[(tt[:, 0] >= t0) & (tt[:, 5] >= t0)]
+        c = {"waves": int(len(tt))}
+        for k in range(1, 6):
+            d = us(tt[:, k] - tt[:, k - 1])
+            c[f"{names[k-1]}->{names[k]}_us"] = {"p50": float(np.median(d)), "max": float(d.max())}
+        for k in range(6):
+            r = us(tt[:, k] - t0)
+            c[f"at_{names[k]}_us"] = {"p50": float(np.median(r)), "max": float(r.max())}
+        out["classes"][cls] = c
+    with open(a.json, "w") as fh:
+        json.dump(out, fh, indent=1)
+    print("wrote", a.json)
 
 
 if __name__ == "__main__":

@@ -26,6 +26,8 @@ __global__ void k_chain(const double *in, double *out, long long *cyc) {
             x = fma(x, e0, e1);
         } else if constexpr (V == 1) {  // forward step: fma(e1, dpp_shr(x), e0 * x)
             x = fma(e1, dpp<0x111>(x), e0 * x);
+        } else if constexpr (V == 7) {  // backward beta step: fma(e0, x, dpp_shl(e1 * x)) (product, then the shift)
+            x = fma(e0, x, dpp<0x101>(e1 * x));
         } else if constexpr (V == 2) {  // two independent forward steps (ILP 2)
             x = fma(e1, dpp<0x111>(x), e0 * x);
             x2 = fma(e1, dpp<0x111>(x2), e0 * x2);
@@ -75,6 +77,7 @@ int main() {
         run<6>("fp32 fma chain (+cvt)", din, dout, dcyc, w);
         run<3>("dpp row_shr 64-bit chain", din, dout, dcyc, w);
         run<1>("forward step (dpp+mul+fma)", din, dout, dcyc, w);
+        run<7>("backward beta step (mul+dpp+fma)", din, dout, dcyc, w);
         run<2>("forward step x2 ILP", din, dout, dcyc, w);
         run<5>("forward step x4 ILP", din, dout, dcyc, w);
     }
