@@ -377,6 +377,35 @@ def engine_waves(R, N, lmap=None):
     return waves, -(-waves // SIMDS), -(-waves // CUS)
 
 
+OPT_ALLREDUCE_KEY = 8  # HMMBW_OPT_ALLREDUCE (include/hmmbw.h): 0 = RCCL / the caller's all-reduce, 1 = peer
+
+
+def torch_allreduce_iteration(eng, dist, device, backend):
+    """One EM iteration through the split ABI with torch.distributed's all-reduce of the statistics in
+    between (hmmbw_iterate_begin -> dist.all_reduce -> hmmbw_iterate_end): the reference path of bench's leg
+    check.  The buffer goes through a torch tensor (device memory for nccl, host for gloo) by hipMemcpy."""
+    import ctypes
+    import torch
+    hip = ctypes.CDLL(os.path.join(os.path.dirname(torch.__file__), "lib", "libamdhip64.so"))
+    hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    ptr, n = eng.iterate_begin()
+    torch.cuda.synchronize()
+    if backend == "nccl":
+        t = torch.empty(n, dtype=torch.float64, device=f"cuda:{device}")
+        assert hip.hipMemcpy(ctypes.c_void_p(t.data_ptr()), ctypes.c_void_p(ptr), 8 * n, 3) == 0
+        dist.all_reduce(t)
+        torch.cuda.synchronize()
+        assert hip.hipMemcpy(ctypes.c_void_p(ptr), ctypes.c_void_p(t.data_ptr()), 8 * n, 3) == 0
+    else:
+        h = np.empty(n, dtype=np.float64)
+        assert hip.hipMemcpy(h.ctypes.data, ctypes.c_void_p(ptr), 8 * n, 2) == 0
+        t = torch.from_numpy(h)
+        dist.all_reduce(t)
+        assert hip.hipMemcpy(ctypes.c_void_p(ptr), h.ctypes.data, 8 * n, 1) == 0
+    torch.cuda.synchronize()
+    eng.iterate_end()
+
+
 def roofline_bounds(R, T, N, kern_s, traffic, issue, estep_s=None, lmap=None, topo=None):
     """Every ceiling that applies to the dominant launch, each as achieved / peak of ONE resource, so every
     frac is <= 1 when the measurement and the model are right; the binding bound is the largest frac.
@@ -738,38 +767,63 @@ def main(argv=None):
         else:
             legs[other] = r2
     agree = None
-    if len(legs) > 1:
-        # both all-reduces must give the same EM run before either is a headline: the same few iterations
-        # from the same parameters on each, L traces (hmm_training.py:503) compared at rtol 1e-9; a leg that
-        # disagrees with RCCL (e.g. a peer exchange that is not coherent over xGMI) is dropped
-        traces = {}
-        for kind in legs:
-            eng.set_allreduce(kind)
+    ref_kind = None
+    if world > 1 and any(k in ("rccl", "peer") for k in legs):
+        # every engine all-reduce must give the same EM run as a reference before it is a headline: the same
+        # few iterations from the same parameters on each, L traces (hmm_training.py:503) compared at rtol
+        # 1e-9.  The reference is the RCCL leg when it ran, else the torch.distributed path (the split ABI
+        # with dist.all_reduce of the statistics in between).  A leg that disagrees (e.g. a peer exchange that
+        # is not coherent over xGMI) is dropped on every rank; if none is left, the torch path is timed.
+        def trace_of(kind):
             eng.set_params(pi, A, B)
-            eng.reset(0.0, 3)
-            eng.enqueue_iterations(3, stats)
             try:
-                traces[kind] = [L for L, _ in eng.status(0, 3)[1]]
+                if kind == "torch":
+                    eng.set_option(OPT_ALLREDUCE_KEY, 0)  # the caller's all-reduce (no peer push)
+                    eng.reset(0.0, 3)
+                    for _ in range(3):
+                        torch_allreduce_iteration(eng, dist, device, args.dist_backend)
+                else:
+                    eng.set_allreduce(kind)
+                    eng.reset(0.0, 3)
+                    eng.enqueue_iterations(3, stats)
+                return [L for L, _ in eng.status(0, 3)[1]]
             except Exception as e:  # noqa: BLE001 - a device-side failure of the check drops that leg
-                traces[kind] = str(e)
-        ref_t = traces.get("rccl")
+                return str(e)
+        ref_kind = "rccl" if "rccl" in legs else "torch"
+        traces = {k: trace_of(k) for k in legs if k in ("rccl", "peer")}
+        if ref_kind == "torch":
+            traces["torch"] = trace_of("torch")
+        ref_t = traces.get(ref_kind)
         agree = {}
         for kind, tr in traces.items():
             ok = isinstance(tr, list) and isinstance(ref_t, list) and np.allclose(tr, ref_t, rtol=1e-9, atol=0.0)
             agree[kind] = bool(ok)
-            if kind != "rccl" and not ok:
-                failed[kind] = f"L trace differs from the RCCL leg's: {tr} vs {ref_t}"
+            if kind in legs and kind != ref_kind and not ok:
+                failed[kind] = f"L trace differs from the {ref_kind} reference's: {tr} vs {ref_t}"
                 legs.pop(kind)
-        if world > 1:  # every rank drops the same legs
-            keep = torch.tensor([1 if k in legs else 0 for k in ("rccl", "peer")], dtype=torch.int32,
-                                device=f"cuda:{device}" if args.dist_backend == "nccl" else "cpu")
-            dist.all_reduce(keep, op=dist.ReduceOp.MIN)
-            for i, k in enumerate(("rccl", "peer")):
-                if k in legs and int(keep[i]) == 0:
-                    legs.pop(k)
-                    failed.setdefault(k, "another rank's check failed")
-        eng.reset(0.0, 1 << 40)
+        # every rank drops the same legs
+        keep = torch.tensor([1 if k in legs else 0 for k in ("rccl", "peer")], dtype=torch.int32,
+                            device=f"cuda:{device}" if args.dist_backend == "nccl" else "cpu")
+        dist.all_reduce(keep, op=dist.ReduceOp.MIN)
+        for i, k in enumerate(("rccl", "peer")):
+            if k in legs and int(keep[i]) == 0:
+                legs.pop(k)
+                failed.setdefault(k, "another rank's check failed")
+        if "rccl" in legs or "peer" in legs:
+            eng.set_allreduce(next(k for k in ("rccl", "peer") if k in legs))
         n_iter[0] = 0
+        if not legs:  # every engine leg dropped: time the torch.distributed path instead (a valid line)
+            eng.set_option(OPT_ALLREDUCE_KEY, 0)
+            eng._native = False
+            stats = eng.make_stats_buffer()
+            eng.reset(0.0, 1 << 40)
+            r3 = leg(args.steps, max(2, min(args.warmup, 10)))
+            if r3["error"]:
+                raise RuntimeError("every all-reduce leg failed: " + json.dumps(failed) + "; torch: " + r3["error"])
+            r3["allreduce"] = None
+            legs["torch"] = r3
+        else:
+            eng.reset(0.0, 1 << 40)
     # the headline is the faster leg (both run the full EM iteration; config.allreduce names it)
     best = max(legs, key=lambda k: -legs[k]["elapsed"])
     L = legs[best]
@@ -872,7 +926,7 @@ def main(argv=None):
                                   "allreduce_us_per_iter": 1000.0 * v["ar_ms"] / v["ar_n"] if v["ar_n"] else None,
                                   "kernel_ms_per_launch_events": v["kern_ms"] / v["kern_n"] if v["kern_n"] else None}
                               for k, v in legs.items()},
-                     "legs_failed": failed, "legs_agree": agree,
+                     "legs_failed": failed, "legs_agree": agree, "legs_reference": ref_kind,
                      "legs_detail": {k: {"payload_bytes": eng.comm_payload_bytes() if eng.native_comm else 8 * eng.stats_len,
                                          "peer_chunks": eng.peer_chunks() if k == "peer" else None,
                                          "peer_flags_written_and_polled_per_rank_per_iter": (

@@ -16,13 +16,13 @@ Kernels small_kernels_n<HMMBW_INST_N>(bool lr, bool ldstab) {
         if (ldstab)
             return Kernels{k_estep_small<N, G, true, true, false>, k_estep_small<N, G, true, true, true>,
                            k_estep_small_group<N, G, true, true, false>, k_estep_small_group<N, G, true, true, true>,
-                           k_estep_small<N, G, true, true, false, true>, k_estep_join<N, G>};
+                           k_estep_small<N, G, true, true, false, true>, k_estep_join<N, G, true>};
         return Kernels{k_estep_small<N, G, true, false, false>, k_estep_small<N, G, true, false, true>};
     }
     if (ldstab)
         return Kernels{k_estep_small<N, G, false, true, false>, k_estep_small<N, G, false, true, true>,
                        k_estep_small_group<N, G, false, true, false>, k_estep_small_group<N, G, false, true, true>,
-                       k_estep_small<N, G, false, true, false, true>};
+                       k_estep_small<N, G, false, true, false, true>, k_estep_join<N, G, false>};
     return Kernels{k_estep_small<N, G, false, false, false>, k_estep_small<N, G, false, false, true>};
 }
 

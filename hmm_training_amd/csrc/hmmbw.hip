@@ -36,6 +36,7 @@
 #include <atomic>
 #include <climits>
 #include <cstdlib>
+#include <cstring>
 #include <map>
 #include <mutex>
 #include <tuple>
@@ -166,6 +167,7 @@ struct PeerArgs {
     long long nch;              // chunks
     int dpt;                    // doubles per thread per chunk (chunk = kPeerThreads x dpt)
     int world, rank;
+    double perturb;             // diagnostics (HMMBW_DIAG_PEER_PERTURB): element 0 of this rank's push x (1 + perturb)
 };
 
 __device__ __forceinline__ unsigned long long *peer_flags(double *region, const PeerArgs &P) {
@@ -178,7 +180,8 @@ __device__ __forceinline__ void peer_push_chunk(const double *src, const PeerArg
     double *dst = P.region[p] + ((long long)(seq & 1) * P.world + P.rank) * P.slot;
     for (int k = 0; k < P.dpt; ++k) {
         const long long i = base + (long long)k * kPeerThreads;
-        if (i < P.n) __hip_atomic_store(dst + i, src[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (i < P.n) __hip_atomic_store(dst + i, i == 0 ? src[i] * (1.0 + P.perturb) : src[i], __ATOMIC_RELAXED,
+                                        __HIP_MEMORY_SCOPE_SYSTEM);
     }
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's write-through stores are acknowledged
     __syncthreads();
@@ -566,6 +569,7 @@ struct hmmbw_ctx {
                                   // dense 0: profiles/r5/spread_knobs.txt); HMMBW_PRIO overrides it
     int split_extra = 1;          // EArgs::split_extra (HMMBW_SPLIT_EXTRA=0 turns it off)
     int join = 1;                 // left-to-right E-step on the joined spread map (k_estep_join; HMMBW_JOIN=0 off)
+    int join_dense = 1;           // the dense E-step on it too (HMMBW_JOIN_DENSE=0 off)
     long long last_nll = 0;       // per-workgroup log-likelihood pairs written by the last E-step launch
     uint16_t *d_sym = nullptr;
     long long *d_wsym = nullptr, *d_wckoff = nullptr, *d_wspoff = nullptr;
@@ -608,7 +612,8 @@ struct hmmbw_ctx {
     int peer_world = 0;
     bool peer_on = false;
     bool peer_revoked = false;
-    bool peer_special = false;    // the region is uncached / fine-grained (HMMBW_PEER_MEM)    // a region this context was attached to was freed by its owner
+    bool peer_special = false;
+    double peer_perturb = 0.0;    // diagnostics: HMMBW_DIAG_PEER_PERTURB=<rank>:<value> (bench's leg check)    // the region is uncached / fine-grained (HMMBW_PEER_MEM)    // a region this context was attached to was freed by its owner
     std::vector<double *> peer_regions;
     std::vector<void *> peer_mapped;
     unsigned long long peer_seq = 0;
@@ -949,9 +954,14 @@ int ensure_wq(hmmbw_ctx *c) {
 // (at most one per CU) becomes waves 4.. of the full workgroup with its index, so each CU runs one 8-wave
 // workgroup: one M-step prologue, one set of LDS tables and one histogram flush instead of two on the CUs
 // that host an extra workgroup.  cfg3: 32.2 -> 30.9 us per iteration (profiles/r5/join_ab.txt).
+// Round 6: the dense E-step joins too (HMMBW_JOIN_DENSE=0 keeps its separate extra workgroups); its split B
+// waves take A's hand-over through an LDS flag, so the joined workgroup's full waves are never held.
 bool joined_map(const hmmbw_ctx *c) {
-    return c->join && !c->wide && !c->det && c->topo == HMMBW_TOPOLOGY_LEFT_TO_RIGHT && c->lds_tables() &&
-           c->nblocks > c->nfull && c->nblocks - c->nfull <= c->nfull && c->xact <= kBlock / kWave;
+    const bool topo_ok = c->topo == HMMBW_TOPOLOGY_LEFT_TO_RIGHT || (c->topo == HMMBW_TOPOLOGY_DENSE && c->join_dense);
+    const int xw = (c->topo == HMMBW_TOPOLOGY_DENSE && c->split_extra && 2 * c->xact <= kBlock / kWave) ? 2 * c->xact
+                                                                                                     : c->xact;
+    return c->join && topo_ok && !c->wide && !c->det && c->lds_tables() && c->nblocks > c->nfull &&
+           c->nblocks - c->nfull <= c->nfull && xw <= kBlock / kWave;
 }
 
 // The dense kernels' split extra waves run (estep_small_body SPLITOK, "split").
@@ -1568,6 +1578,7 @@ int hmmbw_set_observations(hmmbw_ctx *c, const int64_t *offsets, const int32_t *
     if (const char *pe = std::getenv("HMMBW_PRIO")) c->prio = std::atoi(pe);
     if (const char *se = std::getenv("HMMBW_SPLIT_EXTRA")) c->split_extra = std::atoi(se) != 0;
     if (const char *je = std::getenv("HMMBW_JOIN")) c->join = std::atoi(je) != 0;
+    if (const char *jd = std::getenv("HMMBW_JOIN_DENSE")) c->join_dense = std::atoi(jd) != 0;
     long long nfull = nblocks;
     int xact = wpb;
     if (!c->wide && !c->det) {
@@ -1957,6 +1968,7 @@ static PeerArgs peer_args(const hmmbw_ctx *c) {
     P.dpt = c->peer_dpt;
     P.world = c->peer_world;
     P.rank = c->rank;
+    P.perturb = c->peer_perturb;
     return P;
 }
 
@@ -2097,6 +2109,13 @@ static int peer_attach_impl(hmmbw_ctx *c, const std::vector<double *> &regions, 
     c->peer_seq = 0;
     c->peer_on = true;
     c->peer_revoked = false;
+    // diagnostics: one rank pushes a wrong payload, so the exchange disagrees with any other all-reduce
+    // (tests/test_bench.py drives bench.py's leg check with it)
+    c->peer_perturb = 0.0;
+    if (const char *pe = std::getenv("HMMBW_DIAG_PEER_PERTURB")) {
+        const char *colon = std::strchr(pe, ':');
+        if (colon && std::atoi(pe) == c->rank) c->peer_perturb = std::atof(colon + 1);
+    }
     c->R_global = n_seq_global;  // the R of hmm_training.py:424 for hmmbw_iterate's loop
     return HMMBW_OK;
 }

@@ -209,17 +209,69 @@ __device__ __forceinline__ int dpp_i32(int v) {
     return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, true);
 }
 
+// lane ^ 16 / lane ^ 32 partners of a double without LDS: v_permlane16_swap / v_permlane32_swap (VALU) on
+// both halves.  Each returns (own, partner) in an order that depends on the row, so combine the pair with a
+// commutative operation only (every lane of the pair then gets the bitwise-identical result).
+template <bool P32>
+__device__ __forceinline__ void swap_pair(double v, double &a, double &b) {
+    const unsigned lo = (unsigned)__double2loint(v), hi = (unsigned)__double2hiint(v);
+    const auto l = P32 ? __builtin_amdgcn_permlane32_swap(lo, lo, false, false)
+                       : __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+    const auto h = P32 ? __builtin_amdgcn_permlane32_swap(hi, hi, false, false)
+                       : __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+    a = __hiloint2double((int)h[0], (int)l[0]);
+    b = __hiloint2double((int)h[1], (int)l[1]);
+}
+template <bool P32>
+__device__ __forceinline__ double add_swap(double v) {
+    double a, b;
+    swap_pair<P32>(v, a, b);
+    return a + b;
+}
+template <bool P32>
+__device__ __forceinline__ double max_swap(double v) {
+    double a, b;
+    swap_pair<P32>(v, a, b);
+    return fmax(a, b);
+}
+
 // Sum over a group of G lanes (butterfly; every lane gets the bitwise-identical result because
-// each level adds the same two partial sums, only commuted).
+// each level adds the same two partial sums, only commuted).  No LDS round trip: DPP within a row,
+// permlane swaps across rows (round 6: the ds_bpermute of __shfl_xor cost ~120 cycles per level).
 template <int G>
 __device__ __forceinline__ double gsum(double x) {
     if constexpr (G >= 2) x += dpp<0xB1>(x);   // quad_perm [1,0,3,2]
     if constexpr (G >= 4) x += dpp<0x4E>(x);   // quad_perm [2,3,0,1]
     if constexpr (G >= 8) x += dpp<0x141>(x);  // row_half_mirror
     if constexpr (G >= 16) x += dpp<0x140>(x); // row_mirror
-    if constexpr (G >= 32) x += __shfl_xor(x, 16);
-    if constexpr (G >= 64) x += __shfl_xor(x, 32);
+    if constexpr (G >= 32) x = add_swap<false>(x);
+    if constexpr (G >= 64) x = add_swap<true>(x);
     return x;
+}
+
+// Sum over the lanes of a wave that share (lane mod G), e.g. the U sequences of a G-lane-group layout: the
+// result is complete in every lane (the order of the additions may differ between lanes).
+template <int G>
+__device__ __forceinline__ double usum(double x) {
+    if constexpr (G <= 2) x += __shfl_xor(x, 2);
+    if constexpr (G <= 4) x += dpp<0x124>(x);   // row_ror:4
+    if constexpr (G <= 8) x += dpp<0x128>(x);   // row_ror:8
+    if constexpr (G <= 16) x = add_swap<false>(x);
+    return add_swap<true>(x);
+}
+
+// min over the lanes of a wave that share (lane mod G), ints (DPP in the row, permlane swaps across rows)
+template <int G>
+__device__ __forceinline__ int umin_i32(int x) {
+    if constexpr (G <= 2) x = min(x, __shfl_xor(x, 2));
+    if constexpr (G <= 4) x = min(x, dpp_i32<0x124>(x));  // row_ror:4
+    if constexpr (G <= 8) x = min(x, dpp_i32<0x128>(x));  // row_ror:8
+    if constexpr (G <= 16) {
+        const auto r = __builtin_amdgcn_permlane16_swap((unsigned)x, (unsigned)x, false, false);
+        x = min((int)r[0], (int)r[1]);
+    }
+    const auto r = __builtin_amdgcn_permlane32_swap((unsigned)x, (unsigned)x, false, false);
+    return min((int)r[0], (int)r[1]);
 }
 
 template <int G>
@@ -349,16 +401,15 @@ __device__ __forceinline__ char *lds_ptr(unsigned a) {
 
 // Per-block (max, sum exp(x - max)) of the sequences' log P (each sequence contributes from
 // exactly one lane with valid = true).  All threads of the block call it.
+__device__ __forceinline__ double wave_max(double x);
 __device__ __forceinline__ void block_ll_partial(double lp, bool valid, double *sh, double *out) {
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, nw = blockDim.x >> 6;
-    double m = valid ? lp : -INFINITY;
-    for (int k = 32; k >= 1; k >>= 1) m = fmax(m, __shfl_xor(m, k));
+    double m = wave_max(valid ? lp : -INFINITY);
     if (lane == 0) sh[wv] = m;
     __syncthreads();
     double M = -INFINITY;
     for (int w = 0; w < nw; ++w) M = fmax(M, sh[w]);
-    double s = (valid && M != -INFINITY && lp != -INFINITY) ? exp(lp - M) : 0.0;
-    for (int k = 32; k >= 1; k >>= 1) s += __shfl_xor(s, k);
+    const double s = gsum<64>((valid && M != -INFINITY && lp != -INFINITY) ? exp(lp - M) : 0.0);
     __syncthreads();
     if (lane == 0) sh[wv] = s;
     __syncthreads();
@@ -453,7 +504,7 @@ template <int N, int G, bool LR, bool LDSTAB, bool FWD_ONLY, bool DET = false, i
 __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long bid, const long long nblk) {
     static_assert(!DET || (LDSTAB && !FWD_ONLY), "deterministic mode: E-step with LDS tables");
     constexpr bool JOIN = BLK > kBlock;
-    static_assert(!JOIN || (BLK == 2 * kBlock && LR && LDSTAB && !FWD_ONLY && !DET), "joined map: left-to-right E-step");
+    static_assert(!JOIN || (BLK == 2 * kBlock && LDSTAB && !FWD_ONLY && !DET), "joined map: E-step with LDS tables");
     constexpr int U = kWave / G;
     // dense G = 8: xi on the 4x4x4 MFMA (xi_mfma8), two accumulators per lane in its D layout
     constexpr bool XM = !LR && G == 8 && !FWD_ONLY && HMMBW_XI_MFMA;
@@ -471,10 +522,16 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
     // split extra waves possible in this instantiation: dense E-step with LDS tables and atomic statistics
     // (dense cfg3 69.4 -> 64.3 us; left-to-right 34.0 -> 35.6 us, and its code alone costs registers:
     // profiles/r5/split_extra_ab.txt)
-    constexpr bool SPLITOK = (!LR || HMMBW_SPLIT_LR) && LDSTAB && !FWD_ONLY && !DET && !JOIN;
+    // (joined map: the split groups hand over through an LDS flag instead of a workgroup barrier, which would
+    // also hold the full workgroup's waves)
+    constexpr bool SPLITOK = (!LR || HMMBW_SPLIT_LR) && LDSTAB && !FWD_ONLY && !DET;
     extern __shared__ __attribute__((aligned(256))) double smem[];  // 256-B aligned whatever the static LDS (ds_read_b128 rows)
     __shared__ double sPA[G + N * N];  // pi (zero-padded to G) and A of this iteration
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    // joined map, split groups: A's hand-over flags (cleared here; the prologue's barriers order it before use)
+    __shared__ int sXflag[SPLITOK && JOIN ? kBlock / kWave / 2 : 1];
+    if constexpr (SPLITOK && JOIN)
+        if (tid < kBlock / kWave / 2) sXflag[tid] = 0;
     PHASE(0);
     if constexpr (!FWD_ONLY)  // clear the next iteration's statistics (single rank: triple buffer)
         for (long long i = bid * blockDim.x + tid; i < a.zero_len; i += nblk * blockDim.x)
@@ -489,14 +546,16 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
     if constexpr (LDSTAB && !FWD_ONLY) merged = a.merged != 0;
     const int wpb = JOIN ? kBlock / kWave : blockDim.x >> 6;  // waves of a full (sequence-group) workgroup
     const bool xblk = JOIN ? wv >= wpb : bid >= a.nfull;     // this wave runs an extra group
-    // split extra waves: in an extra workgroup with 2 xact <= 4 waves, wave wv in [xact, 2 xact) is the B
-    // partner of wave wv - xact (same sequence group): it runs the lower half of the group's backward
+    const int wx = JOIN ? wv - wpb : wv;                      // index among the extra group's waves
+    // split extra waves: with 2 xact <= 4 extra waves, extra wave wx in [xact, 2 xact) is the B partner of extra
+    // wave wx - xact (same sequence group): it runs the lower half of the group's backward
     const bool split_wg = SPLITOK && xblk && a.split_extra != 0 && 2 * a.xact <= wpb;
-    const bool brole = split_wg && wv >= a.xact && wv < 2 * a.xact;
+    const bool brole = split_wg && wx >= a.xact && wx < 2 * a.xact;
     const int wvg = brole ? wv - a.xact : wv;
-    const long long wave = JOIN ? (xblk ? a.nfull * wpb + bid * a.xact + (wv - wpb) : bid * wpb + wv)
+    const int xs = JOIN ? wvg - wpb : wvg;                    // the group's hand-over slot
+    const long long wave = JOIN ? (xblk ? a.nfull * wpb + bid * a.xact + (wvg - wpb) : bid * wpb + wv)
                                 : (xblk ? a.nfull * wpb + (bid - a.nfull) * a.xact + wvg : bid * wpb + wv);
-    const bool wactive = !xblk || (JOIN ? wv - wpb : wv) < a.xact || brole;
+    const bool wactive = !xblk || wx < a.xact || brole;
     if (merged) {
         // the previous iteration's M-step, computed redundantly by every workgroup straight into
         // its LDS tables (no separate M-step kernel, no parameter round trip through HBM)
@@ -573,8 +632,7 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
         // z starts at 0 in the (masked) first chunk and their beta at 1/P = 0, so every term they
         // add in an unmasked chunk is an exact zero.
         int Tmin = T > 0 ? T : INT_MAX;
-#pragma unroll
-        for (int m = G; m < kWave; m <<= 1) Tmin = min(Tmin, __shfl_xor(Tmin, m));
+        Tmin = umin_i32<G>(Tmin);
 
         // transition coefficients of this lane (state j)
         double acol[LR ? 1 : N], arow[LR ? 1 : N];
@@ -876,16 +934,29 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
             double bt = 0.0;
             if (brole && spl) bt = presweep(hc * kChunk, Eb);
             if (!brole && spl) {
-                sXinv[wvg][lane] = alive ? 1.0 / phat : 0.0;
-                sXd[wvg][lane] = C - Ch;
-                if (lane == 0) sXsafe[wvg] = safe ? 1 : 0;
+                sXinv[xs][lane] = alive ? 1.0 / phat : 0.0;
+                sXd[xs][lane] = C - Ch;
+                if (lane == 0) sXsafe[xs] = safe ? 1 : 0;
             }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-            __syncthreads();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            if constexpr (JOIN) {
+                // A releases its slot's flag; B waits for it (the full waves of the workgroup are not held)
+                if (!brole && spl) {
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                    if (lane == 0) __hip_atomic_store(&sXflag[xs], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
+                if (brole && spl) {
+                    while (__hip_atomic_load(&sXflag[xs], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0)
+                        __builtin_amdgcn_s_sleep(1);
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                }
+            } else {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                __syncthreads();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            }
             if (brole && spl) {
-                safe = sXsafe[wvg] != 0;
-                beta_h = __builtin_amdgcn_ldexp(bt, Eb - sXd[wvg][lane]) * sXinv[wvg][lane];
+                safe = sXsafe[xs] != 0;
+                beta_h = __builtin_amdgcn_ldexp(bt, Eb - sXd[xs][lane]) * sXinv[xs][lane];
             }
         }
 
@@ -1194,7 +1265,7 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
                 }
             }
         }
-    } else if (split_wg) {  // no sequence group here: the split barrier still counts every wave
+    } else if (split_wg && !JOIN) {  // no sequence group here: the split barrier still counts every wave
         __syncthreads();
     }
 
@@ -1237,15 +1308,11 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
         vals[NSR + 1] = gall;
         vals[NSR + 2] = pin;
 #pragma unroll
-        for (int k = K0; k < NV; ++k) {
-            double x = vals[k];
-            for (int m = G; m < kWave; m <<= 1) x += __shfl_xor(x, m);
-            vals[k] = x;
-        }
+        for (int k = K0; k < NV; ++k) vals[k] = usum<G>(vals[k]);
         double xd = 0.0, xo = 0.0;
         if constexpr (XM) {  // sum the two seq parities (lane bit 3)
-            xd = S[0] + __shfl_xor(S[0], 8);
-            xo = S[1] + __shfl_xor(S[1], 8);
+            xd = S[0] + dpp<0x128>(S[0]);  // row_ror:8 = lane ^ 8 within the row
+            xo = S[1] + dpp<0x128>(S[1]);
         }
         __syncthreads();
         if (u == 0) {
@@ -1308,11 +1375,12 @@ __global__ void __launch_bounds__(kBlock, 2) k_estep_small(EArgs a) {  // 2 wave
     estep_small_body<N, G, LR, LDSTAB, FWD_ONLY, DET>(a, blockIdx.x, gridDim.x);
 }
 
-// Joined spread map (left-to-right E-step with LDS tables): one 8-wave workgroup per CU, grid = nfull;
-// waves 4.. of workgroup b run extra workgroup b's xact sequence groups (estep_small_body, JOIN).
-template <int N, int G>
+// Joined spread map (E-step with LDS tables): one 8-wave workgroup per CU, grid = nfull; waves 4.. of
+// workgroup b run extra workgroup b's xact sequence groups (estep_small_body, JOIN), and on the dense path
+// their split B partners (hand-over by LDS flag).
+template <int N, int G, bool LR>
 __global__ void __launch_bounds__(2 * kBlock, 1) k_estep_join(EArgs a) {
-    estep_small_body<N, G, true, true, false, false, 2 * kBlock>(a, blockIdx.x, gridDim.x);
+    estep_small_body<N, G, LR, true, false, false, 2 * kBlock>(a, blockIdx.x, gridDim.x);
 }
 
 // Grouped launch: g.nm models of one shape (same N, topology and tables), model m owning workgroups
@@ -1337,20 +1405,14 @@ __global__ void __launch_bounds__(kBlock, 2) k_estep_small_group(GroupArgs g) {
 // ---------------------------------------------------------------------------------------------
 __device__ double block_reduce(double x, double *sh, bool is_max) {
     const int tid = threadIdx.x;
-    for (int m = 32; m >= 1; m >>= 1) {
-        const double y = __shfl_xor(x, m);
-        x = is_max ? fmax(x, y) : x + y;
-    }
+    x = is_max ? wave_max(x) : gsum<64>(x);
     __syncthreads();
     if ((tid & 63) == 0) sh[tid >> 6] = x;
     __syncthreads();
     if (tid < 64) {
         const int nw = blockDim.x >> 6;
         double y = tid < nw ? sh[tid] : (is_max ? -INFINITY : 0.0);
-        for (int m = 32; m >= 1; m >>= 1) {
-            const double z = __shfl_xor(y, m);
-            y = is_max ? fmax(y, z) : y + z;
-        }
+        y = is_max ? wave_max(y) : gsum<64>(y);
         if (tid == 0) sh[0] = y;
     }
     __syncthreads();
@@ -1681,8 +1743,8 @@ __device__ __forceinline__ double wave_max(double x) {
     x = fmax(x, dpp<0x4E>(x));
     x = fmax(x, dpp<0x141>(x));
     x = fmax(x, dpp<0x140>(x));
-    x = fmax(x, __shfl_xor(x, 16));
-    return fmax(x, __shfl_xor(x, 32));
+    x = max_swap<false>(x);
+    return max_swap<true>(x);
 }
 
 // Multi-rank fused E-step (hmmbw_iterate with the engine communicator): the workgroups accumulate

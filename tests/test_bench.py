@@ -74,7 +74,7 @@ def test_bench_single_gpu_line():
     assert rf["frac"] == pytest.approx(rf["achieved"] / rf["peak"])
     # the tightest ceiling the counters measure: achieved / peak of one resource, so <= 1, with provenance
     bd = rf["bounds"]
-    assert rf["binding"]["resource"] == bd["binding"] in ("hbm", "valu", "simd_valu", "cu_lds")
+    assert rf["binding"]["resource"] == bd["binding"] in ("hbm", "valu", "simd_valu", "cu_lds", "latency", "phase_model")
     assert 0 < rf["binding"]["frac"] <= 1.0
     assert rf["binding"]["frac"] == max(b["frac"] for b in bd.values() if isinstance(b, dict) and "frac" in b)
     # the busiest SIMD and CU on the engine's spread map: cfg3's 1,250 waves = 256 full workgroups + 113 of 2
@@ -113,6 +113,28 @@ def test_bench_self_spawned_two_ranks_one_gpu_gloo():
     assert d["comm"]["rccl_comm_ranks"] == 0 and d["synced"]["dropin_iterations"] == 20
     # gloo has no RCCL communicator: the engine's own peer all-reduce (IPC handles over gloo) runs the loop
     assert d["comm"]["kind"] == "peer" and d["comm"]["legs"]["peer"]["allreduce_us_per_iter"] > 0
+    # without RCCL the peer leg is checked against the torch.distributed path before it may be the headline
+    assert d["comm"]["legs_reference"] == "torch" and d["comm"]["legs_agree"]["peer"] is True
+
+
+@pytest.mark.gpu
+def test_bench_drops_a_peer_leg_that_disagrees():
+    """The guard the first 8-GPU run depends on (hmm_training.py:503, L over all ranks): rank 1 pushes a wrong
+    payload into the peer exchange (HMMBW_DIAG_PEER_PERTURB), so the peer leg's L trace disagrees with the
+    torch.distributed reference; bench.py must drop the leg on every rank, report it in legs_failed, and still
+    print a valid line timed on the torch path."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["HMMBW_DIAG_PEER_PERTURB"] = "1:0.001"
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--steps", "5", "--warmup", "1", "--R", "2000",
+                        "--dist-backend", "gloo", "--no-cpu-baseline", "--no-synced"], cwd=ROOT, capture_output=True,
+                       text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _json_line(r.stdout)
+    c = d["comm"]
+    assert "peer" in c["legs_failed"] and "differs" in c["legs_failed"]["peer"]
+    assert c["legs_agree"] == {"peer": False, "torch": True} and c["legs_reference"] == "torch"
+    assert c["kind"] == "torch" and "peer" not in c["legs"] and d["value"] > 0 and d["n_gpus"] == 2
+    assert d["config"]["allreduce"].startswith("torch.distributed")
 
 
 @pytest.mark.gpu

@@ -378,17 +378,21 @@ def test_spread_extra_waves_ragged_vs_oracle(oracle_mt, monkeypatch, xact, topol
     assert np.isclose(StatsLayout.lse_of_pairs(g["ll_pairs"]), oracle_mt.lse(s.logP), rtol=1e-12)
 
 
+@pytest.mark.parametrize("join", ["1", "0"])
 @pytest.mark.parametrize("split", ["0", "1"])
 @pytest.mark.parametrize("T,topology,safe", [(203, "left_to_right", False), (203, "dense", False), (9, "left_to_right", False),
-                                             (64, "left_to_right", True), (96, "dense", True)])
-def test_split_extra_waves_vs_oracle(oracle_mt, monkeypatch, split, T, topology, safe):
+                                             (64, "left_to_right", True), (96, "dense", True), (9, "dense", False)])
+def test_split_extra_waves_vs_oracle(oracle_mt, monkeypatch, split, T, topology, safe, join):
     """Split extra waves (HMMBW_SPLIT_EXTRA, estep_small_body "split"): 10,000 equal-length sequences put a
     second wave on 226 SIMDs; with the split each such group's backward is cut at chunk nch / 2 and its idle
     partner wave runs the lower half from its own beta pre-sweep, rescaled into the forward's scaling.
     Odd T (a partial top chunk), the two-chunk minimum (T = 9), per-step (safe) scaling, both topologies:
-    2 EM iterations and every statistic against the oracle (hmm_training.py:351-514)."""
+    2 EM iterations and every statistic against the oracle (hmm_training.py:351-514).  join: the joined spread map
+    (one 8-wave workgroup per CU, round 6 for the dense kernel: the split groups hand over by an LDS flag) or
+    the separate extra workgroups (HMMBW_JOIN_DENSE=0 / HMMBW_JOIN=0)."""
     from hmm_training_amd.engine import BaumWelchEngine
     monkeypatch.setenv("HMMBW_SPLIT_EXTRA", split)
+    monkeypatch.setenv("HMMBW_JOIN_DENSE" if topology == "dense" else "HMMBW_JOIN", join)
     R, N, K, iters = 10_000, 8, 256, 2
     sym = _symbols(R, T, N, K, "U", 71 + T)
     off = np.arange(R + 1, dtype=np.int64) * T
@@ -397,6 +401,9 @@ def test_split_extra_waves_vs_oracle(oracle_mt, monkeypatch, split, T, topology,
     with BaumWelchEngine(N, K, topology=topology, safe_scaling=safe) as eng:
         eng.set_observations(offsets=off, symbols=sym)
         eng.set_params(pi, A, B)
+        lm = eng.launch_map()
+        assert bool(lm["joined"]) == (join == "1"), lm
+        assert bool(lm["split_extra"]) == (split == "1" and topology == "dense"), lm
         eng.reset(0.0, iters)
         eng.enqueue_iterations(iters)
         st, recs = eng.status(0, iters)
