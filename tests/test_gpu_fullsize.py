@@ -333,12 +333,12 @@ def test_cfg5_whole_iteration_vs_oracle(oracle_mt, cfg5_whole_gpu):
 @pytest.mark.parametrize("xact,topology,join", [(None, "left_to_right", None), ("1", "left_to_right", None),
                                                 ("3", "left_to_right", None), ("4", "left_to_right", None),
                                                 (None, "left_to_right", "0"), ("1", "left_to_right", "0"),
-                                                (None, "dense", None)])
+                                                (None, "dense", None), (None, "dense", "0")])
 def test_spread_extra_waves_ragged_vs_oracle(oracle_mt, monkeypatch, xact, topology, join):
     """More waves than SIMDs (9,000 ragged sequences = 1,125 waves on 1,024 SIMDs): one full workgroup
     per CU, then workgroups of xact active waves (default 2; HMMBW_XACT forces 1, 3 or 4 = no spread map),
-    with inactive waves in them; left-to-right by default on the joined map (the extra workgroups' waves as
-    waves 4.. of the full ones, k_estep_join), HMMBW_JOIN=0 the separate workgroups; every statistic and
+    with inactive waves in them; by default on the joined map (the extra workgroups' waves as waves 4.. of the
+    full ones, k_estep_join; dense too since round 6), HMMBW_JOIN=0 the separate workgroups; every statistic and
     the trained model against the oracle (hmm_training.py:351-514)."""
     from hmm_training_amd.engine import BaumWelchEngine, StatsLayout, to_csr
     if xact is not None:
@@ -357,7 +357,7 @@ def test_spread_extra_waves_ragged_vs_oracle(oracle_mt, monkeypatch, xact, topol
         lm = eng.launch_map()
         spread = xact != "4"
         assert (lm["workgroups"] > lm["full_workgroups"]) == spread, lm
-        assert lm["joined"] == (spread and topology == "left_to_right" and join != "0"), lm
+        assert lm["joined"] == (spread and join != "0"), lm  # round 6: the dense E-step joins too
         eng.reset(0.0, iters)
         eng.enqueue_iterations(iters)
         st, recs = eng.status(0, iters)
