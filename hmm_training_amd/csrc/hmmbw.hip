@@ -1024,7 +1024,7 @@ int plan_estep(hmmbw_ctx *c, bool fwd_only, const IterState *state, double *copi
                 p.grid = (unsigned)c->nfull;
                 p.nll = c->nfull;
                 p.block = 2 * kBlock;
-                p.lds = sizeof(double) * (tabs + (size_t)(2 * wpb) * c->G * NV + 8);
+                p.lds = sizeof(double) * (tabs + (size_t)(2 * wpb) * c->G * NV + 16);  // + [8 waves][2] LL pairs
             }
             if (HMMBW_ZFULL && !lr && !fwd_only) {  // dense: the forward stores every z_t (hmmbw_device.hpp)
                 if (int rc = ensure_zf(c)) return rc;

@@ -489,6 +489,7 @@ template <int N, int G, int GP, bool PT, int BLK = kBlock>
 __device__ __forceinline__ bool merged_mstep(const EArgs &a, double *sP, double *sH, double *sPA, long long bid);
 __device__ __forceinline__ int rank_ll_count(const EArgs &a);
 __device__ __forceinline__ void rank_ll_fold(const EArgs &a, long long nblk);
+__device__ __forceinline__ void ll_merge(double &M, double &S, double m2, double s2);
 
 // Body of the small-N E-step / scorer for workgroup `bid` of the `nblk` workgroups that cover one
 // model's sequences: the whole grid of k_estep_small, or one model's slice of a grouped launch
@@ -1289,15 +1290,51 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
         }
     }
     PHASE(11);
-    // per-block (max, sum exp) of log P for the convergence scalar
-    block_ll_partial(logp_lane, ll_valid, sRed, a.llpart + 2 * bid);
+    // per-block (max, sum exp) of log P for the convergence scalar.  E-step (round 6): each wave forms its own
+    // (max, sum exp) pair and writes it beside its statistics partials, and thread 0 merges the waves' pairs
+    // after the one barrier the statistics need anyway (block_ll_partial took three more).
+    const int nwv = blockDim.x >> 6;
+    double *sLL = sRed + (size_t)(BLK / kWave) * G * NV;  // [waves][2] (the host sizes the scratch)
+    if constexpr (FWD_ONLY) {
+        block_ll_partial(logp_lane, ll_valid, sRed, a.llpart + 2 * bid);
+    } else {
+        const double wm = wave_max(ll_valid ? logp_lane : -INFINITY);
+        const double ws = gsum<64>((ll_valid && wm != -INFINITY && logp_lane != -INFINITY) ? exp(logp_lane - wm) : 0.0);
+        if (lane == 0) {
+            sLL[2 * wv] = wm;
+            sLL[2 * wv + 1] = ws;
+        }
+    }
     PHASE(4);
     // fused multi-rank launch: thread 0 counts this workgroup's pair in during the statistics flush (the
     // ticket's round trip overlaps the flush), and wave 0 of the last one folds the pairs at the end
     const bool fused_ll = !FWD_ONLY && !DET && a.rank_ll != nullptr;
     int ticket = 0;
     bool counted = false;
+    // the waves' log-likelihood pairs merged by wave 0 (after the barrier below), lane w taking wave w's pair:
+    // one exp per lane in parallel (a serial merge by one thread put ~0.5 us on the tail)
+    auto ll_out = [&]() {
+        if (wv == 0) {
+            double mw = -INFINITY, sw = 0.0;
+            if (lane < nwv) {
+                mw = sLL[2 * lane];
+                sw = sLL[2 * lane + 1];
+            }
+            const bool ok = sw > 0.0;
+            const double M = wave_max(ok ? mw : -INFINITY);
+            const double S = gsum<64>((ok && M != -INFINITY) ? sw * exp(mw - M) : 0.0);
+            // memory-side atomics: the fused M-step of the last workgroup reads these with atomics too
+            if (lane == 0) {
+                atomicExch(&a.llpart[2 * bid], (S > 0.0) ? M : 0.0);
+                atomicExch(&a.llpart[2 * bid + 1], S);
+            }
+        }
+    };
 
+    if constexpr (!FWD_ONLY) if (a.ablate & 1) {
+        __syncthreads();
+        ll_out();
+    }
     if constexpr (!FWD_ONLY) if (!(a.ablate & 1)) {
         // ---- reduce per-lane accumulators over the U sequences of the wave, then the block ----
         constexpr int K0 = XM ? NSR : 0;  // XM: the S columns come from the MFMA lanes below
@@ -1314,7 +1351,6 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
             xd = S[0] + dpp<0x128>(S[0]);  // row_ror:8 = lane ^ 8 within the row
             xo = S[1] + dpp<0x128>(S[1]);
         }
-        __syncthreads();
         if (u == 0) {
 #pragma unroll
             for (int k = K0; k < NV; ++k) sRed[(wv * G + j) * NV + k] = vals[k];
@@ -1334,6 +1370,7 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
         if constexpr (DET)
             for (long long i = tid; i < a.off_bnum; i += blockDim.x) sPart[i] = 0.0;
         __syncthreads();
+        ll_out();
         if (fused_ll && tid == 0) ticket = rank_ll_count(a);
         counted = true;
         const int nw = blockDim.x >> 6;

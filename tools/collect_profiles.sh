@@ -12,7 +12,7 @@ cp "$SRC/calib_WRITE_SIZE/run_counter_collection.csv" "profiles/$DEST/pmc_calib_
 declare -A KEY=([lr_cfg3]=R10000_T200_N8_K256_left_to_right [lrH_cfg3]=R10000_T200_N8_K256_left_to_right_H
                 [dense_cfg3]=R10000_T200_N8_K256_dense [cfg5]=R6250_T400_N64_K1024_dense
                 [cfg4shard]=R12500_T200_N8_K256_left_to_right)
-declare -A KER=([lr_cfg3]=k_estep_join [lrH_cfg3]=k_estep_join [dense_cfg3]=k_estep_small
+declare -A KER=([lr_cfg3]=k_estep_join [lrH_cfg3]=k_estep_join [dense_cfg3]=k_estep_join
                 [cfg5]="k_estep_mfma,k_bnum_gather" [cfg4shard]=k_estep_join)
 for W in lr_cfg3 lrH_cfg3 dense_cfg3 cfg5 cfg4shard; do
   [ -d "$SRC/trace_$W" ] || { echo "skip $W (not in this run)"; continue; }
