@@ -468,6 +468,25 @@ constexpr int kTabPad = HMMBW_TAB_PAD;
 #ifndef HMMBW_SPLIT_LR  // split extra waves in the left-to-right kernels too (A/B builds)
 #define HMMBW_SPLIT_LR 0
 #endif
+#ifndef HMMBW_KARG_TOUCH  // touch every line of the kernel arguments at entry, in one batch (round 6 A/B)
+#define HMMBW_KARG_TOUCH 1
+#endif
+
+// The prologue reads the kernel arguments in several dependent rounds (the zero loop's, then the M-step's, then
+// the launch map's), and the first read of each 64-B line of the argument segment misses the scalar cache:
+// ~0.4 us per round at cfg3 (phase stamps, profiles/r6/phase_lr_cfg3.json).  One load per line, all issued
+// before the first wait, makes it one miss latency: LR cfg3 29.72 -> 29.62 us, T = 8 13.69 -> 13.56
+// (profiles/r6/prologue_ab.txt).
+template <class Args>
+__device__ __forceinline__ void touch_kernargs() {
+    typedef const __attribute__((address_space(4))) unsigned karg_u32;
+    karg_u32 *p = (karg_u32 *)__builtin_amdgcn_kernarg_segment_ptr();
+    constexpr int n = (int)((sizeof(Args) + 63) / 64);
+    unsigned acc = 0;
+#pragma unroll
+    for (int i = 0; i < n; ++i) acc ^= p[i * 16];
+    asm volatile("" ::"s"(acc));
+}
 constexpr int kHistOff = kTabPad ? 40960 : 32768;
 __host__ __device__ constexpr bool lds_tables_fit(int K, int GP) { return (size_t)K * GP * 16 <= (size_t)kHistOff; }
 __host__ __device__ constexpr size_t lds_table_bytes(int K, int GP) { return (size_t)kHistOff + (size_t)K * GP * 16; }
@@ -1409,6 +1428,9 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
 
 template <int N, int G, bool LR, bool LDSTAB, bool FWD_ONLY, bool DET = false>
 __global__ void __launch_bounds__(kBlock, 2) k_estep_small(EArgs a) {  // 2 waves per SIMD (<= 256 VGPRs)
+#if HMMBW_KARG_TOUCH
+    touch_kernargs<EArgs>();
+#endif
     estep_small_body<N, G, LR, LDSTAB, FWD_ONLY, DET>(a, blockIdx.x, gridDim.x);
 }
 
@@ -1417,6 +1439,9 @@ __global__ void __launch_bounds__(kBlock, 2) k_estep_small(EArgs a) {  // 2 wave
 // their split B partners (hand-over by LDS flag).
 template <int N, int G, bool LR>
 __global__ void __launch_bounds__(2 * kBlock, 1) k_estep_join(EArgs a) {
+#if HMMBW_KARG_TOUCH
+    touch_kernargs<EArgs>();
+#endif
     estep_small_body<N, G, LR, true, false, false, 2 * kBlock>(a, blockIdx.x, gridDim.x);
 }
 
@@ -1841,22 +1866,13 @@ __device__ __forceinline__ bool merged_mstep(const EArgs &a, double *sP, double 
     const int K = a.K;
     const long long len = m.copy_len;
     PHASE(8);
-    // ---- every load issued before any use: statistics, log-likelihood pairs, convergence state ----
+    // ---- every load issued before any use: statistics, log-likelihood pairs, convergence state (the
+    // pairs and the state before the other copies' statistics are waited for: one latency, not two) ----
     double v[SB];
 #pragma unroll
     for (int q = 0; q < SB; ++q) {
         const long long idx = (long long)q * BLK + tid;
         v[q] = m.src[idx < len ? idx : len - 1];
-    }
-    for (int c = 1; c < m.nsrc; ++c) {
-        double x[SB];
-#pragma unroll
-        for (int q = 0; q < SB; ++q) {
-            const long long idx = (long long)q * BLK + tid;
-            x[q] = m.src[c * len + (idx < len ? idx : len - 1)];
-        }
-#pragma unroll
-        for (int q = 0; q < SB; ++q) v[q] += x[q];
     }
     const long long nb = m.nblocks;  // >= 1
     double pm[PB], ps[PB];
@@ -1879,6 +1895,16 @@ __device__ __forceinline__ bool merged_mstep(const EArgs &a, double *sP, double 
         in.error_src = m.state->error_src;
         in.last_L = m.state->last_L;
         in.last_diff = m.state->last_diff;
+    }
+    for (int c = 1; c < m.nsrc; ++c) {
+        double x[SB];
+#pragma unroll
+        for (int q = 0; q < SB; ++q) {
+            const long long idx = (long long)q * BLK + tid;
+            x[q] = m.src[c * len + (idx < len ? idx : len - 1)];
+        }
+#pragma unroll
+        for (int q = 0; q < SB; ++q) v[q] += x[q];
     }
     PHASE_DRAIN(9);
     // ---- L = LSE_r log P_r (:503) in two passes: max, then sum of exp(m - max) ----
