@@ -964,10 +964,11 @@ bool joined_map(const hmmbw_ctx *c) {
            c->nblocks - c->nfull <= c->nfull && xw <= kBlock / kWave;
 }
 
-// The dense kernels' split extra waves run (estep_small_body SPLITOK, "split").
+// The split extra waves run (estep_small_body SPLITOK, "split"): dense, and left-to-right on the joined map.
 bool split_extra_map(const hmmbw_ctx *c) {
-    return c->split_extra && !c->wide && !c->det && c->topo == HMMBW_TOPOLOGY_DENSE && c->lds_tables() &&
-           c->nblocks > c->nfull && 2 * c->xact <= kBlock / kWave;
+    const bool topo_ok = c->topo == HMMBW_TOPOLOGY_DENSE || (c->topo == HMMBW_TOPOLOGY_LEFT_TO_RIGHT && joined_map(c));
+    return c->split_extra && !c->wide && !c->det && topo_ok && c->lds_tables() && c->nblocks > c->nfull &&
+           2 * c->xact <= kBlock / kWave;
 }
 
 int plan_estep(hmmbw_ctx *c, bool fwd_only, const IterState *state, double *copies, double *llpart, double *zero,
@@ -1026,6 +1027,10 @@ int plan_estep(hmmbw_ctx *c, bool fwd_only, const IterState *state, double *copi
                 p.block = 2 * kBlock;
                 p.lds = sizeof(double) * (tabs + (size_t)(2 * wpb) * c->G * NV + 16);  // + [8 waves][2] LL pairs
             }
+            // left-to-right: split extra waves on the joined map only (round 6, cfg3 29.63 -> 28.33 us,
+            // profiles/r6/split_lr_ab.txt); beside separate extra workgroups they cost more than they save
+            // (round 5: 34.0 -> 35.6 us)
+            if (lr && p.fn != ks.join_estep) a.split_extra = 0;
             if (HMMBW_ZFULL && !lr && !fwd_only) {  // dense: the forward stores every z_t (hmmbw_device.hpp)
                 if (int rc = ensure_zf(c)) return rc;
                 a.ckpt = c->d_zf;

@@ -465,8 +465,8 @@ constexpr int kTabPad = HMMBW_TAB_PAD;
 #ifndef HMMBW_FLUSH_VMWAIT  // explicit vmcnt(0) before the histogram flush (round 6 A/B)
 #define HMMBW_FLUSH_VMWAIT 1
 #endif
-#ifndef HMMBW_SPLIT_LR  // split extra waves in the left-to-right kernels too (A/B builds)
-#define HMMBW_SPLIT_LR 0
+#ifndef HMMBW_SPLIT_LR  // split extra waves in the left-to-right kernels too (the host enables them on the joined map)
+#define HMMBW_SPLIT_LR 1
 #endif
 #ifndef HMMBW_KARG_TOUCH  // touch every line of the kernel arguments at entry, in one batch (round 6 A/B)
 #define HMMBW_KARG_TOUCH 1
@@ -540,11 +540,12 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
     // left-to-right with LDS tables: per (symbol, state) products {a_jj b_j(o), a_{j-1,j} b_j(o)}
     constexpr bool PT = LR && LDSTAB;
     // split extra waves possible in this instantiation: dense E-step with LDS tables and atomic statistics
-    // (dense cfg3 69.4 -> 64.3 us; left-to-right 34.0 -> 35.6 us, and its code alone costs registers:
-    // profiles/r5/split_extra_ab.txt)
+    // (dense cfg3 69.4 -> 64.3 us), left-to-right on the joined map only (round 6: cfg3 29.63 -> 28.33 us,
+    // profiles/r6/split_lr_ab.txt; beside separate extra workgroups 34.0 -> 35.6 us and its code costs
+    // registers, profiles/r5/split_extra_ab.txt)
     // (joined map: the split groups hand over through an LDS flag instead of a workgroup barrier, which would
     // also hold the full workgroup's waves)
-    constexpr bool SPLITOK = (!LR || HMMBW_SPLIT_LR) && LDSTAB && !FWD_ONLY && !DET;
+    constexpr bool SPLITOK = (!LR || (HMMBW_SPLIT_LR && JOIN)) && LDSTAB && !FWD_ONLY && !DET;
     extern __shared__ __attribute__((aligned(256))) double smem[];  // 256-B aligned whatever the static LDS (ds_read_b128 rows)
     __shared__ double sPA[G + N * N];  // pi (zero-padded to G) and A of this iteration
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;

@@ -403,7 +403,8 @@ def test_split_extra_waves_vs_oracle(oracle_mt, monkeypatch, split, T, topology,
         eng.set_params(pi, A, B)
         lm = eng.launch_map()
         assert bool(lm["joined"]) == (join == "1"), lm
-        assert bool(lm["split_extra"]) == (split == "1" and topology == "dense"), lm
+        # left-to-right splits on the joined map only (round 6)
+        assert bool(lm["split_extra"]) == (split == "1" and (topology == "dense" or join == "1")), lm
         eng.reset(0.0, iters)
         eng.enqueue_iterations(iters)
         st, recs = eng.status(0, iters)
@@ -420,24 +421,26 @@ def test_split_extra_waves_vs_oracle(oracle_mt, monkeypatch, split, T, topology,
     assert_stats(g, s, R, T)
 
 
+@pytest.mark.parametrize("topology", ["dense", "left_to_right"])
 @pytest.mark.parametrize("N,R", [(4, 20_000), (5, 10_000), (12, 5_000), (16, 5_000)])
-def test_split_extra_waves_other_group_sizes_vs_oracle(oracle_mt, monkeypatch, N, R):
-    """The split extra waves at the other lane-group sizes of the dense kernel (G = 4, 8 with padding
-    states, 16): R chosen so that the sequence groups overflow the 1,024 SIMDs by ~22 % (the spread map's
-    extra workgroups), T = 72 (9 chunks, an odd count), 2 EM iterations and every statistic against the
-    oracle (hmm_training.py:351-514)."""
+def test_split_extra_waves_other_group_sizes_vs_oracle(oracle_mt, monkeypatch, N, R, topology):
+    """The split extra waves at the other lane-group sizes (G = 4, 8 with padding states, 16), dense and
+    left-to-right (the joined map): R chosen so that the sequence groups overflow the 1,024 SIMDs by ~22 %
+    (the spread map's extra workgroups), T = 72 (9 chunks, an odd count), 2 EM iterations and every statistic
+    against the oracle (hmm_training.py:351-514)."""
     from hmm_training_amd.engine import BaumWelchEngine
     monkeypatch.setenv("HMMBW_SPLIT_EXTRA", "1")
     T, K, iters = 72, 64, 2
     sym = _symbols(R, T, N, K, "U", 90 + N)
     off = np.arange(R + 1, dtype=np.int64) * T
-    pi, A, B = _params(N, K, "dense", 90 + N)
+    pi, A, B = _params(N, K, topology, 90 + N)
     ref = oracle_mt.hmm_training(off, sym.astype(np.int64), N, K, 0.0, iters, pi, A, B)
-    with BaumWelchEngine(N, K, topology="dense") as eng:
+    with BaumWelchEngine(N, K, topology=topology) as eng:
         eng.set_observations(offsets=off, symbols=sym)
         eng.set_params(pi, A, B)
         lm = eng.launch_map()
         assert lm["extra_waves"] in (1, 2) and lm["workgroups"] > lm["full_workgroups"], lm
+        assert lm["split_extra"], lm
         eng.reset(0.0, iters)
         eng.enqueue_iterations(iters)
         st, recs = eng.status(0, iters)

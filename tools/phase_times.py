@@ -118,7 +118,8 @@ def run_one(a, R, torch, BaumWelchEngine, default_initial_params, out_dir):
 def write_json(a, R, eng, l, us):
     """Phase durations by SIMD class on the engine's launch map (bench.py's phase model reads this): `busy` =
     the waves on SIMDs that hold two sequence-group waves (joined map: full waves 0 .. xact-1 and extra waves
-    4 .. 3+xact of the workgroups that carry extra groups), `lone` = the other full waves.  Stamps are indexed
+    4 .. 3+xact of the workgroups that carry extra groups; with split extra groups every full wave of those
+    workgroups, their A and B waves in classes of their own), `lone` = the other full waves.  Stamps are indexed
     by (workgroup, wave) of the launched kernel: 8 waves per workgroup on the joined map."""
     import json
     import time
@@ -136,11 +137,21 @@ def write_json(a, R, eng, l, us):
     assert l.hmmbw_debug_phase_times(buf.ctypes.data, n) == 0
     t = buf[:nwg * wpw].astype(np.int64)
     t0 = t[t[:, 0] > 0, 0].min()
-    busy, lone = [], []
+    split = joined and bool(m.get("split_extra"))
+    busy, lone, split_a, split_b = [], [], [], []
     for b in range(nwg):
         for wv in range(wpw):
             idx = b * wpw + wv
-            if joined:
+            if joined and split and b < nx_wg:
+                # split extra groups: A waves 4 .. 3+xact (SIMDs 0 ..), B waves 4+xact .. 3+2 xact; every full
+                # wave of the workgroup shares its SIMD with one of them
+                if wv < 4:
+                    busy.append(idx)
+                elif wv < 4 + xact:
+                    split_a.append(idx)
+                elif wv < 4 + 2 * xact:
+                    split_b.append(idx)
+            elif joined:
                 if b < nx_wg and (wv < xact or 4 <= wv < 4 + xact):
                     busy.append(idx)
                 elif wv < 4:
@@ -152,7 +163,7 @@ def write_json(a, R, eng, l, us):
            "collected_utc": time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime()),
            "span_us": float(us(t[:, 5].max() - t0)), "classes": {}}
     names = ["start", "tables", "forward", "backward", "ll", "flush"]
-    for cls, ids in (("busy", busy), ("lone", lone)):
+    for cls, ids in (("busy", busy), ("lone", lone), ("split_a", split_a), ("split_b", split_b)):
         if not ids:
             continue
         tt = t[ids]
