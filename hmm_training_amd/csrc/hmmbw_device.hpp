@@ -30,6 +30,16 @@ static __device__ unsigned long long g_phase[kPhaseWaves][kPhaseSlots];
         const long long w_ = (long long)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);   \
         if ((threadIdx.x & 63) == 0 && w_ < kPhaseWaves) g_phase[w_][k] = wall_clock64();      \
     } while (0)
+// diagnostics: where the wave runs: HW_ID (wave, SIMD, CU, shader array, engine fields) in slot 15, XCC_ID
+// in slot 14
+#define PHASE_HWID()                                                                                    \
+    do {                                                                                                \
+        const long long w_ = (long long)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);            \
+        if ((threadIdx.x & 63) == 0 && w_ < kPhaseWaves) {                                              \
+            g_phase[w_][15] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);                      \
+            g_phase[w_][14] = (unsigned)__builtin_amdgcn_s_getreg((15 << 11) | 20);                     \
+        }                                                                                               \
+    } while (0)
 // diagnostics: wait for every outstanding memory operation of the wave, then stamp
 #define PHASE_DRAIN(k)                   \
     do {                                 \
@@ -56,6 +66,9 @@ static __device__ unsigned long long g_chunk[4096][2][64];
     } while (0)
 #define PHASE(k) \
     do {         \
+    } while (0)
+#define PHASE_HWID() \
+    do {             \
     } while (0)
 #define PHASE_DRAIN(k) \
     do {               \
@@ -554,6 +567,7 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
     if constexpr (SPLITOK && JOIN)
         if (tid < kBlock / kWave / 2) sXflag[tid] = 0;
     PHASE(0);
+    PHASE_HWID();
     if constexpr (!FWD_ONLY)  // clear the next iteration's statistics (single rank: triple buffer)
         for (long long i = bid * blockDim.x + tid; i < a.zero_len; i += nblk * blockDim.x)
             a.zero[i] = 0.0;
@@ -897,12 +911,13 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
                     body(c + 3, I0{}, F0{}, F0{});
                 }
             }
-            for (; c + 4 <= lim; c += 4) {
-                body(c, I1{}, Mk{}, F0{});
-                body(c + 1, I2{}, Mk{}, F0{});
-                body(c + 2, I3{}, Mk{}, F0{});
-                body(c + 3, I0{}, Mk{}, F0{});
-            }
+            auto trip = [&](int c0) {
+                body(c0, I1{}, Mk{}, F0{});
+                body(c0 + 1, I2{}, Mk{}, F0{});
+                body(c0 + 2, I3{}, Mk{}, F0{});
+                body(c0 + 3, I0{}, Mk{}, F0{});
+            };
+            for (; c + 4 <= lim; c += 4) trip(c);
             if (c < nch) {
                 tail_body(c, I1{});
                 if (c + 1 < nch) {
@@ -1237,12 +1252,13 @@ __device__ __forceinline__ void estep_small_body(const EArgs &a, const long long
                             body(c - 3, I0{}, U0{});
                         }
                     }
-                    for (; c >= clo + 3; c -= 4) {
-                        body(c, I1{}, Mk{});
-                        body(c - 1, I2{}, Mk{});
-                        body(c - 2, I3{}, Mk{});
-                        body(c - 3, I0{}, Mk{});
-                    }
+                    auto trip = [&](int c0) {
+                        body(c0, I1{}, Mk{});
+                        body(c0 - 1, I2{}, Mk{});
+                        body(c0 - 2, I3{}, Mk{});
+                        body(c0 - 3, I0{}, Mk{});
+                    };
+                    for (; c >= clo + 3; c -= 4) trip(c);
                     if (c >= clo) {
                         body(c, I1{}, Mk{});
                         if (c - 1 >= clo) {

@@ -176,6 +176,19 @@ def write_json(a, R, eng, l, us):
             r = us(tt[:, k] - t0)
             c[f"at_{names[k]}_us"] = {"p50": float(np.median(r)), "max": float(r.max())}
         out["classes"][cls] = c
+    # where the waves ran (slot 15 = HW_ID: SIMD bits 5:4, CU bits 11:8, shader array 12, engine 15:13; slot 14 = XCC)
+    hw = t[:, 15]
+    if np.any(hw):
+        simd = (hw >> 4) & 3
+        cu = (hw >> 8) & 15
+        maps = {}
+        for b in range(min(nwg, 512)):
+            key = tuple(int(x) for x in simd[b * wpw:(b + 1) * wpw])
+            maps[key] = maps.get(key, 0) + 1
+        out["wave_simd_maps"] = [{"simd_of_wave": list(k), "workgroups": v} for k, v in sorted(maps.items(), key=lambda kv: -kv[1])]
+        same_cu = sum(1 for b in range(nwg) if len(set(int(x) for x in cu[b * wpw:(b + 1) * wpw])) == 1)
+        out["workgroups_on_one_cu"] = same_cu
+        print("wave -> SIMD maps of the workgroups (count):", out["wave_simd_maps"][:4])
     with open(a.json, "w") as fh:
         json.dump(out, fh, indent=1)
     print("wrote", a.json)
