@@ -32,13 +32,16 @@ def main():
     ap.add_argument("--kwaves", type=int, default=0, help="kernel waves to read (default: R / sequences per wave)")
     ap.add_argument("--lib", default=None, help="prebuilt diagnostics library (default hmm_training_amd/libhmmbw_phase.so)")
     ap.add_argument("--json", default=None, help="write the per-class phase summary (busy / lone SIMDs) here")
+    ap.add_argument("--chunks", action="store_true", help="also stamp every chunk (-DHMMBW_CHUNK_TIMES; per-class chunk cycles)")
     a = ap.parse_args()
     out_dir = os.path.join(ROOT, "gpurun_out", "phase")
     os.makedirs(out_dir, exist_ok=True)
-    lib = a.lib or os.path.join(ROOT, "hmm_training_amd", "libhmmbw_phase.so")  # prebuilt in-tree if present
+    name = "libhmmbw_chunk.so" if a.chunks else "libhmmbw_phase.so"
+    lib = a.lib or os.path.join(ROOT, "hmm_training_amd", name)  # prebuilt in-tree if present
     if not os.path.exists(lib):
         from hmm_training_amd import build as B
-        B.build(force=True, defines=["-DHMMBW_PHASE_TIMES"], out=lib, tag="phase")
+        defs = ["-DHMMBW_PHASE_TIMES"] + (["-DHMMBW_CHUNK_TIMES"] if a.chunks else [])
+        B.build(force=True, defines=defs, out=lib, tag="chunk" if a.chunks else "phase")
     os.environ["HMMBW_LIB"] = lib
     import torch
     from hmm_training_amd.engine import BaumWelchEngine
@@ -176,6 +179,28 @@ def write_json(a, R, eng, l, us):
             r = us(tt[:, k] - t0)
             c[f"at_{names[k]}_us"] = {"p50": float(np.median(r)), "max": float(r.max())}
         out["classes"][cls] = c
+    # per-class chunk cycles (chunk-stamp build): forward chunk c -> c+1, backward chunk c -> c-1 (descending)
+    nck = n if n <= 4096 else 4096
+    ck = np.zeros((4096, 2, 64), dtype=np.uint64)
+    if hasattr(l, "hmmbw_debug_chunk_times"):
+        l.hmmbw_debug_chunk_times.argtypes = [ctypes.c_void_p, ctypes.c_int64]
+        if l.hmmbw_debug_chunk_times(ck.ctypes.data, 4096) == 0 and np.any(ck):
+            ck = ck.astype(np.int64)
+            nch = (a.T + 7) // 8
+            out["chunk_cycles"] = {}
+            for cls, ids in (("busy", busy), ("lone", lone), ("split_a", split_a), ("split_b", split_b)):
+                ids = [i for i in ids if i < nck and np.all(ck[i, 0, :nch] > 0)]
+                if not ids:
+                    continue
+                f = np.diff(ck[ids, 0, :nch], axis=1)
+                b = ck[ids, 1, :nch]
+                db = b[:, :-1] - b[:, 1:]  # chunk c's stamp is later than chunk c + 1's
+                ok = (b[:, :-1] > 0) & (b[:, 1:] > 0)
+                out["chunk_cycles"][cls] = {
+                    "waves": len(ids),
+                    "forward_p50_per_chunk": [float(np.median(f[:, c])) for c in range(f.shape[1])],
+                    "backward_p50_per_chunk": [float(np.median(db[ok[:, c], c])) if ok[:, c].any() else None
+                                               for c in range(db.shape[1])]}
     # where the waves ran (slot 15 = HW_ID: SIMD bits 5:4, CU bits 11:8, shader array 12, engine 15:13; slot 14 = XCC)
     hw = t[:, 15]
     if np.any(hw):
