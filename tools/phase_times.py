@@ -142,6 +142,7 @@ def write_json(a, R, eng, l, us):
     t0 = t[t[:, 0] > 0, 0].min()
     split = joined and bool(m.get("split_extra"))
     busy, lone, split_a, split_b = [], [], [], []
+    busy_a, busy_b = [], []  # split: the full waves that share a SIMD with an A wave / with a B wave (waves w, w + 4)
     for b in range(nwg):
         for wv in range(wpw):
             idx = b * wpw + wv
@@ -150,6 +151,10 @@ def write_json(a, R, eng, l, us):
                 # wave of the workgroup shares its SIMD with one of them
                 if wv < 4:
                     busy.append(idx)
+                    if wv < xact:
+                        busy_a.append(idx)
+                    elif wv < 2 * xact:
+                        busy_b.append(idx)
                 elif wv < 4 + xact:
                     split_a.append(idx)
                 elif wv < 4 + 2 * xact:
@@ -166,7 +171,8 @@ def write_json(a, R, eng, l, us):
            "collected_utc": time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime()),
            "span_us": float(us(t[:, 5].max() - t0)), "classes": {}}
     names = ["start", "tables", "forward", "backward", "ll", "flush"]
-    for cls, ids in (("busy", busy), ("lone", lone), ("split_a", split_a), ("split_b", split_b)):
+    for cls, ids in (("busy", busy), ("lone", lone), ("split_a", split_a), ("split_b", split_b),
+                     ("busy_with_a", busy_a), ("busy_with_b", busy_b)):
         if not ids:
             continue
         tt = t[ids]
