@@ -570,6 +570,7 @@ struct hmmbw_ctx {
     int split_extra = 1;          // EArgs::split_extra (HMMBW_SPLIT_EXTRA=0 turns it off)
     int join = 1;                 // left-to-right E-step on the joined spread map (k_estep_join; HMMBW_JOIN=0 off)
     int join_dense = 1;           // the dense E-step on it too (HMMBW_JOIN_DENSE=0 off)
+    bool fits_cus = false;        // the launch map's workgroups fit one per CU (set_observations)
     long long last_nll = 0;       // per-workgroup log-likelihood pairs written by the last E-step launch
     uint16_t *d_sym = nullptr;
     long long *d_wsym = nullptr, *d_wckoff = nullptr, *d_wspoff = nullptr;
@@ -956,11 +957,18 @@ int ensure_wq(hmmbw_ctx *c) {
 // that host an extra workgroup.  cfg3: 32.2 -> 30.9 us per iteration (profiles/r5/join_ab.txt).
 // Round 6: the dense E-step joins too (HMMBW_JOIN_DENSE=0 keeps its separate extra workgroups); its split B
 // waves take A's hand-over through an LDS flag, so the joined workgroup's full waves are never held.
+#ifndef HMMBW_JOIN_ALL
+#define HMMBW_JOIN_ALL 1
+#endif
 bool joined_map(const hmmbw_ctx *c) {
     const bool topo_ok = c->topo == HMMBW_TOPOLOGY_LEFT_TO_RIGHT || (c->topo == HMMBW_TOPOLOGY_DENSE && c->join_dense);
     const int xw = (c->topo == HMMBW_TOPOLOGY_DENSE && c->split_extra && 2 * c->xact <= kBlock / kWave) ? 2 * c->xact
                                                                                                      : c->xact;
-    return c->join && topo_ok && !c->wide && !c->det && c->lds_tables() && c->nblocks > c->nfull &&
+    // Round 6: left-to-right without extra groups too (at most 4 groups per CU, one workgroup per CU), the idle waves
+    // 4-7 then only sharing the prologue's table build and the flush: T = 8 at 8,192 sequences 13.51 -> 12.96 us,
+    // 8,192 x 200 27.59 -> 27.32, 4,096 x 200 24.30 -> 23.72 (profiles/r6/join_all_ab.txt)
+    const bool all = HMMBW_JOIN_ALL && c->topo == HMMBW_TOPOLOGY_LEFT_TO_RIGHT && c->nblocks == c->nfull && c->fits_cus;
+    return c->join && topo_ok && !c->wide && !c->det && c->lds_tables() && (c->nblocks > c->nfull || all) &&
            c->nblocks - c->nfull <= c->nfull && xw <= kBlock / kWave;
 }
 
@@ -1694,6 +1702,11 @@ int hmmbw_set_observations(hmmbw_ctx *c, const int64_t *offsets, const int32_t *
     c->nwaves = nwaves;
     c->nblocks = nblocks;
     c->nfull = nfull;
+    {
+        int ncu = 0;
+        (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device);
+        c->fits_cus = ncu > 0 && nblocks <= ncu;
+    }
     c->xact = xact;
     c->has_obs = true;
     if (int rc2 = ensure_wq(c)) return rc2;

@@ -378,6 +378,47 @@ def test_spread_extra_waves_ragged_vs_oracle(oracle_mt, monkeypatch, xact, topol
     assert np.isclose(StatsLayout.lse_of_pairs(g["ll_pairs"]), oracle_mt.lse(s.logP), rtol=1e-12)
 
 
+@pytest.mark.parametrize("R,join", [(8192, None), (3001, None), (8192, "0")])
+def test_joined_map_without_extra_groups_vs_oracle(oracle_mt, monkeypatch, R, join):
+    """Round 6: with at most 4 sequence groups per CU (no spread map) the left-to-right E-step still runs the joined
+    kernel, one 8-wave workgroup per CU whose waves 4-7 hold no group and only share the table build and the flush
+    (HMMBW_JOIN=0: the plain 4-wave workgroups).  R = 8,192 (every SIMD one group) and 3,001 ragged (a partial last
+    workgroup); 2 EM iterations and every statistic against the oracle (hmm_training.py:351-514)."""
+    from hmm_training_amd.engine import BaumWelchEngine, StatsLayout, to_csr
+    if join is not None:
+        monkeypatch.setenv("HMMBW_JOIN", join)
+    rng = np.random.default_rng(R)
+    N, K, iters = 8, 256, 2
+    obs = [rng.integers(0, K, size=int(t)) for t in rng.integers(40, 120, size=R)]
+    off, sym = to_csr(obs)
+    pi, A, B = _params(N, K, "left_to_right", 17)
+    ref = oracle_mt.hmm_training(off, sym.astype(np.int64), N, K, 0.0, iters, pi, A, B)
+    with BaumWelchEngine(N, K, topology="left_to_right") as eng:
+        eng.set_observations(obs)
+        eng.set_params(pi, A, B)
+        lm = eng.launch_map()
+        assert lm["workgroups"] == lm["full_workgroups"] and not lm["split_extra"], lm
+        assert lm["joined"] == (join != "0"), lm
+        eng.reset(0.0, iters)
+        eng.enqueue_iterations(iters)
+        st, recs = eng.status(0, iters)
+        np.testing.assert_allclose([L for L, _ in recs], ref.trace_L, rtol=LL_RTOL)
+        np.testing.assert_allclose(eng.loglik(), ref.logP, rtol=LL_RTOL)
+        p_out, A_out, B_out = eng.params(normalise=True)
+        p_cur, A_cur, B_cur = eng.params(normalise=False)
+        g, ll, _ = statistics_pass(eng, N, K, R)
+    assert_params(A_out, ref.A, "A")
+    assert_params(B_out, ref.B, "B")
+    assert_params(p_out, ref.pi, "pi")
+    s = oracle_mt.estep_logstats(off, sym.astype(np.int64), N, K, p_cur, A_cur, B_cur)
+    np.testing.assert_allclose(ll, s.logP, rtol=LL_RTOL)
+    with np.errstate(under="ignore"):
+        for key, lkey in (("pi_num", "log_pi_num"), ("xi", "log_xi"), ("gamma_den_excl", "log_gden_excl"),
+                          ("gamma_den_all", "log_gden_all"), ("B_num", "log_bnum")):
+            np.testing.assert_allclose(g[key], np.exp(getattr(s, lkey)), rtol=STAT_RTOL, atol=1e-300, err_msg=key)
+    assert np.isclose(StatsLayout.lse_of_pairs(g["ll_pairs"]), oracle_mt.lse(s.logP), rtol=1e-12)
+
+
 @pytest.mark.parametrize("join", ["1", "0"])
 @pytest.mark.parametrize("split", ["0", "1"])
 @pytest.mark.parametrize("T,topology,safe", [(203, "left_to_right", False), (203, "dense", False), (9, "left_to_right", False),

@@ -5,7 +5,8 @@ interleaved in rounds so that every variant sees the same box and clocks.
 (';' separates library specs when one carries several settings: --libs 'libhmmbw.so;libhmmbw.so:A=1,B=2')
 
 cases: lr (cfg3 left-to-right), lrH (cfg3 skewed symbols), dense (cfg3 dense), cfg4 (the 12,500 shard),
-t8 (T = 8 at 8,192 sequences: the fixed cost per launch), cfg5 (the wide shard, 6,250 x 400).
+t8 (T = 8 at 8,192 sequences: the fixed cost per launch), cfg5 (the wide shard, 6,250 x 400), r8k / r4k (8,192 /
+4,096 sequences at T = 200: one sequence group per SIMD / on every other SIMD, no extra groups).
 Prints one line per (round, case, lib) and a median summary per (case, lib)."""
 import argparse
 import json
@@ -22,6 +23,8 @@ CASES = {
     "cfg4": ["--workload", "cfg4"],
     "t8": ["--R", "8192", "--T", "8"],
     "cfg5": ["--workload", "cfg5"],
+    "r8k": ["--R", "8192"],
+    "r4k": ["--R", "4096"],
 }
 
 
